@@ -1,0 +1,172 @@
+/*
+ * rt/rt.h — C-ABI of the MI355X path-tracing render path (librt_hip.so).
+ *
+ * This is the drop-in boundary for the reference's per-pixel render loop:
+ *
+ *   rt_fill_canva   replaces fill_canva(void*)            main.c:245-284
+ *                   (same pthread start-routine signature, same ThreadData
+ *                    layout; main.c:446 only swaps the function name)
+ *   rt_render_rows  replaces the thread-spawn loop        main.c:402-453
+ *                   and the CUDA staging + launch         main_cuda.cu:280-339
+ *                   (state init :326, render_canva<<<>>> :329, D2H :332-339)
+ *   rt_render_async device-resident twin of render_canva  main_cuda.cu:143-171
+ *                   (caller-owned device frame, caller's HIP stream)
+ *
+ * Plain C types only: pointers, sizes and the reference-shaped structs of
+ * rt/types.h.  All entry points return RT_OK (0) or a negative RT_E* code and
+ * never exit(); the message of the last failure on the calling thread is
+ * rt_last_error().
+ */
+#ifndef RT_RT_H
+#define RT_RT_H
+
+#include "types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------- */
+#define RT_OK            0
+#define RT_EINVAL       -1   /* bad argument (sizes, NULL, out-of-range index) */
+#define RT_EDEVICE      -2   /* HIP runtime / device failure                   */
+#define RT_ENOMEM       -3   /* host or device allocation failed                */
+#define RT_EUNSUPPORTED -4   /* valid request the GPU path does not implement   */
+
+/* ---- random-number streams ---------------------------------------------- */
+/* RT_RNG_PHILOX: draw n of sample s at pixel p is word (n & 3) of
+ * Philox4x32-10(key = seed, counter = {n >> 2, 0, p, s}) >> 1, i.e. the
+ * hiprand/rocrand `rocrand_init(seed, (s << 32) | p, 0)` stream truncated to
+ * the 31 bits glibc rand() returns (rtutility.h:229-231 semantics otherwise).
+ * RT_RNG_GLIBC: one sequential glibc rand() stream (the reference's own);
+ * inherently serial, so only the CPU oracle implements it.                  */
+#define RT_RNG_PHILOX 0
+#define RT_RNG_GLIBC  1
+
+/* ---- scene: the reference's arrays, unchanged --------------------------- */
+typedef struct rt_scene {
+    const rt_sphere*   sphere_list;    int nbSpheres;      /* main.c:332-347      */
+    const rt_triangle* triangle_list;  int nbTriangles;    /* mesh.h:96-218       */
+    const rt_material* mat_list;       /* texel table, nbMaterials*th*tw, texture.h:175 */
+    int tex_width, tex_height, nbMaterials;
+    const int*         quelMatPourTri; /* per-triangle material, mesh.h:172        */
+} rt_scene;
+
+/* ---- render parameters (main.c:293-347 constants, ThreadData fields) ---- */
+typedef struct rt_params {
+    int largeur_image, hauteur_image;  /* W, H                                   */
+    int nbRayonParPixel;               /* samples per pixel S (>= 1)             */
+    int nbRebondMax;                   /* bounce budget B (>= 0)                 */
+    rt_camera cam;                     /* from init_camera, camera.h:21-40       */
+    double focus_distance;
+    double ouverture_x, ouverture_y;   /* aperture (depth of field)              */
+    double AO_intensity;
+    int useAO;
+    int compat_int_truncation;         /* 1: truncate focus/ouverture/AO to int
+                                          as ThreadData does (main.c:42-43)      */
+    int rng;                           /* RT_RNG_*                               */
+    int reserved0;
+    unsigned long long seed;           /* Philox key                             */
+} rt_params;
+
+/* Fills defaults: RT_RNG_PHILOX, seed 1010 (main_cuda.cu's curand seed),
+ * compat_int_truncation 1, everything else zero. */
+void rt_params_init(rt_params* p);
+
+/* ---- lifecycle ---------------------------------------------------------- */
+/* Devices used by rt_render_rows / rt_fill_canva (row tiles are dealt
+ * cyclically over them).  ndev <= 0 or devices == NULL selects device 0.
+ * Calling any render entry point without rt_init implies rt_init(0, NULL). */
+int  rt_init(int ndev, const int* devices);
+void rt_shutdown(void);
+const char* rt_last_error(void);
+const char* rt_version(void);
+int  rt_device_count(void);
+
+/* ---- host-buffer drop-in ------------------------------------------------ */
+/* Renders rows row_hi down to row_lo (inclusive; row 0 = bottom, pixel
+ * index j*W+i as main.c:261) into caller-owned arrays of W*H colors.  canva
+ * receives write_color_canva() values (ints 0..255 stored as double,
+ * rtutility.h:56-71); albedo/normal receive the per-pixel means
+ * (main.c:278-279).  albedo/normal may be NULL.  Only the named rows are
+ * written.  Thread-safe for concurrent calls on disjoint rows. */
+int rt_render_rows(const rt_scene* scene, const rt_params* params,
+                   int row_hi, int row_lo,
+                   rt_color* canva, rt_color* albedo, rt_color* normal);
+
+/* pthread start routine with fill_canva's exact contract (main.c:245-284):
+ * arg is a struct ThreadData / rt_thread_data.  Renders start_row..end_row
+ * on the GPU with the Philox stream (seed 1010).  Returns NULL on success,
+ * (void*)1 on failure (see rt_last_error on that thread). */
+void* rt_fill_canva(void* thread_data);
+
+/* ---- device-resident interface ------------------------------------------ */
+typedef struct rt_device_scene rt_device_scene;   /* opaque */
+
+int  rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out);
+void rt_scene_release(rt_device_scene* scene);
+
+/* Which rows one launch renders.  Local tile lt in [0, n_tiles) is global
+ * tile t = tile_first + lt*tile_step, covering global rows
+ * row_base + t*tile_rows + y, y in [0, tile_rows); rows >= H are skipped.
+ * Output row lt*tile_rows + y of the frame buffers holds that global row.
+ * A contiguous band [lo, hi] is {lo, hi-lo+1, 0, 1, 1}; rank r of G with
+ * cyclic k-row tiles is {0, k, r, G, ceil(ceil(H/k)/G)}. */
+typedef struct rt_tiling {
+    int row_base, tile_rows, tile_first, tile_step, n_tiles;
+} rt_tiling;
+
+/* Device pointers, each n_tiles*tile_rows*W colors (double3).  canva is
+ * required; albedo, normal and radiance (pre-gamma mean, sum/S) optional. */
+typedef struct rt_frame {
+    rt_color* canva;
+    rt_color* albedo;
+    rt_color* normal;
+    rt_color* radiance;
+} rt_frame;
+
+/* Enqueue the render on `hip_stream` (hipStream_t, NULL = null stream).
+ * Asynchronous: returns after the launch. */
+int rt_render_async(const rt_device_scene* scene, const rt_params* params,
+                    const rt_tiling* tiling, const rt_frame* frame,
+                    void* hip_stream);
+
+/* Un-permute a rank-major gather of per-rank frames into a full W*H plane.
+ * gathered: world * rows_per_rank * W colors, rank r's block rendered with
+ * tiling {0, tile_rows, r, world, rows_per_rank/tile_rows}.  out: W*H. */
+int rt_assemble_async(const rt_color* gathered, int world, int tile_rows,
+                      int rows_per_rank, int W, int H, rt_color* out,
+                      void* hip_stream);
+
+/* ---- instrumentation (roofline accounting, tests) ----------------------- */
+enum {
+    RT_CNT_SAMPLES = 0,   /* camera samples traced                         */
+    RT_CNT_CASTS,         /* closest-hit casts (bounce + AO)               */
+    RT_CNT_SPHERE_TESTS,  /* ray-sphere tests                              */
+    RT_CNT_SPHERE_DISC,   /* ... with discriminant > 0                     */
+    RT_CNT_TRI_TESTS,     /* ray-triangle tests                            */
+    RT_CNT_SHADE,         /* direction samples (random_dir_no_norm calls)  */
+    RT_CNT_TEX_HITS,      /* closest hits on a triangle (texel fetch)      */
+    RT_CNT_REFRACT,       /* refraction-branch events                      */
+    RT_CNT_RNG_DRAWS,     /* 31-bit draws consumed                         */
+    RT_NCOUNTERS
+};
+/* Same traversal as rt_render_async, no frame; adds event counts into the
+ * device array d_counters[RT_NCOUNTERS] (unsigned long long). */
+int rt_count_async(const rt_device_scene* scene, const rt_params* params,
+                   const rt_tiling* tiling, unsigned long long* d_counters,
+                   void* hip_stream);
+
+/* Device-math self test: evaluates one device primitive on n host inputs
+ * (synchronous, device 0).  op: 0 acos, 1 sinf, 2 cosf, 3 pow(x, y),
+ * 4 sqrt, 5 x/y, 6 sqrtf, 7 philox word (in[0..3] = ctr, in[4..5] = key as
+ * integers in doubles; returns 4 words per input).  Inputs are read as pairs
+ * (x, y) for binary ops. */
+int rt_selftest_math(int op, const double* in, double* out, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_RT_H */

@@ -1,0 +1,90 @@
+"""Benchmark / parity scenes, as the reference's own data.
+
+The Cornell box is README.md:46-59's `sphere_list` (the 4-field material
+initialisers of main_cuda.cu's material), extended with alpha = 1.0 and
+materialIndex = 1.0 so it is visible to main.c's 6-field material
+(hitinfo.h:6-13; with alpha = 0 every non-emitter would be an alpha hole,
+main.c:200-206).  Camera: README.md:14-22.  See SURVEY.md §8 "Config
+resolution".
+"""
+import json
+import os
+import ctypes as C
+
+from .types import Vec3, Material, Sphere, Triangle, UV, Camera
+
+RED, GREEN, BLUE = (1, 0, 0), (0, 1, 0), (0, 0, 1)
+WHITE, BLACK, SKY = (1, 1, 1), (0, 0, 0), (0.784, 0.965, 1)
+
+# (center, radius, diffuse, emission, emissionStrength, reflectionStrength)
+README_SPHERES = [
+    ((-501, 0, 0), 500, GREEN, BLACK, 0.0, 0.96),
+    ((0, -501, 0), 500, WHITE, BLACK, 0.0, 0.0),
+    ((501, 0, 0), 500, RED, BLACK, 0.0, 0.96),
+    ((-0.5, 1.4, -1.2), 0.5, BLACK, (1.0, 0.6, 0.2), 4.0, 0.0),     # orange
+    ((0.5, 1.4, -2.2), 0.5, BLACK, (0.7, 0.2, 1.0), 4.0, 0.0),      # violet
+    ((0.6, -1.4, -1.0), 0.5, BLACK, (0.55, 0.863, 1.0), 2.5, 0.0),  # light blue
+    ((-0.5, -1.4, -3.1), 0.5, BLACK, (0.431, 1.0, 0.596), 2.5, 0.0),  # light green
+    ((0, 0, -504), 500, WHITE, BLACK, 0.0, 0.0),
+    ((0, 501, 0), 500, WHITE, BLACK, 0.0, 0.0),
+    ((0.4, -0.5, -3.3), 0.5, SKY, BLACK, 0.0, 0.99),
+]
+
+README_CAMERA = dict(origin=(0.34, 0.3, 0.5), target=(0.0, -0.5, -3.0), up=(0, 1, 0),
+                     vfov=70.0, ratio=4.0 / 3.0, focus=3.0, aperture=(0.0, 0.0))
+
+
+def material(diffuse, emission=BLACK, es=0.0, refl=0.0, alpha=1.0, ior=1.0):
+    m = Material()
+    m.diffuseColor = Vec3(*diffuse)
+    m.emissionColor = Vec3(*emission)
+    m.emissionStrength, m.reflectionStrength = es, refl
+    m.alpha, m.materialIndex = alpha, ior
+    return m
+
+
+def cornell_spheres(alpha=1.0, material_index=1.0, extra=()):
+    """README 10-sphere box; `extra` appends (center, r, Material) tuples."""
+    rows = list(README_SPHERES)
+    arr = (Sphere * (len(rows) + len(extra)))()
+    for k, (c, r, d, e, es, rf) in enumerate(rows):
+        arr[k].center = Vec3(*c)
+        arr[k].radius = r
+        arr[k].mat = material(d, e, es, rf, alpha, material_index)
+    for k, (c, r, m) in enumerate(extra):
+        arr[len(rows) + k].center = Vec3(*c)
+        arr[len(rows) + k].radius = r
+        arr[len(rows) + k].mat = m
+    return arr
+
+
+def image_height(width, ratio=4.0 / 3.0):
+    """main.c:295: hauteur_image = (int)(largeur_image / ratio)."""
+    return int(width / ratio)
+
+
+_GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                       "tests", "golden")
+
+
+def load_mesh_fixture(name):
+    """Load a mesh fixture (triangles, per-triangle material, texel table)
+    written by tests/golden/make_fixtures.py from the reference loaders.
+    Returns (triangles, quelMatPourTri, mat_list, tw, th, n_materials)."""
+    with open(os.path.join(_GOLDEN, "scenes", name + ".json")) as f:
+        d = json.load(f)
+    tris = d["triangles"]
+    arr = (Triangle * len(tris))()
+    for k, t in enumerate(tris):
+        arr[k].A, arr[k].B, arr[k].C = Vec3(*t["A"]), Vec3(*t["B"]), Vec3(*t["C"])
+        arr[k].uvA, arr[k].uvB, arr[k].uvC = UV(*t["uvA"]), UV(*t["uvB"]), UV(*t["uvC"])
+        arr[k].mat = material(SKY, BLACK, 0.0, 0.0, 0.0, 0.0)   # mesh.h:206
+    qm = (C.c_int * len(tris))(*d["quelMatPourTri"])
+    tex = d["texels"]
+    mats = (Material * len(tex))()
+    for k, (r, g, b, a) in enumerate(tex):
+        # texture.h:233-246: diffuse = P3/maxval, alpha = first channel/maxval,
+        # emissionStrength = 0; emissionColor/reflectionStrength/materialIndex
+        # are never written by the reference loader (read as 0).
+        mats[k] = material((r, g, b), BLACK, 0.0, 0.0, a, 0.0)
+    return arr, qm, mats, d["tex_width"], d["tex_height"], d["n_materials"]
