@@ -24,6 +24,9 @@
 
 #ifdef __cplusplus
 extern "C" {
+#define RT_BOOL bool
+#else
+#define RT_BOOL _Bool
 #endif
 
 typedef struct rt_vec3 { double e[3]; } rt_vec3;
@@ -83,7 +86,7 @@ typedef struct rt_thread_data {
     int nbSpheres, nbTriangles;
     int ouverture_x, ouverture_y, focus_distance;
     int AO_intensity;
-    _Bool useAO;
+    RT_BOOL useAO;
 } rt_thread_data;
 
 #ifdef __cplusplus

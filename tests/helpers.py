@@ -1,0 +1,81 @@
+"""Shared scene builders and oracle/product drivers for the tests."""
+import ctypes as C
+import hashlib
+
+import numpy as np
+
+import oracle_ffi
+import tipe_rt
+from tipe_rt import scenes
+from tipe_rt.types import Vec3, Scene, Params, RT_RNG_PHILOX, RT_RNG_GLIBC, RT_NCOUNTERS
+
+
+def readme_camera_oracle():
+    cam = scenes.README_CAMERA
+    return oracle_ffi.oracle().oracle_init_camera(Vec3(*cam["origin"]), Vec3(*cam["target"]), Vec3(*cam["up"]),
+                                                  cam["vfov"], cam["ratio"])
+
+
+class SceneBundle:
+    """Keeps the ctypes arrays alive next to the rt_scene that points at them."""
+
+    def __init__(self, spheres=None, mesh=None):
+        self.spheres = spheres
+        self.mesh = mesh
+        if mesh is not None:
+            tris, qm, mats, tw, th, nm = mesh
+            self.scene = tipe_rt.make_scene(spheres, tris, qm, mats, tw, th, nm)
+        else:
+            self.scene = tipe_rt.make_scene(spheres)
+
+
+def cornell(extra=()):
+    return SceneBundle(scenes.cornell_spheres(extra=extra))
+
+
+def pyramid_scene(move=(-0.6, -1.0, -2.0)):
+    tris, qm, mats, tw, th, nm = scenes.load_mesh_fixture("pyramide")
+    for t in tris:
+        for P in (t.A, t.B, t.C):
+            P.e[0] += move[0]
+            P.e[1] += move[1]
+            P.e[2] += move[2]
+    return SceneBundle(scenes.cornell_spheres(), (tris, qm, mats, tw, th, nm))
+
+
+def params(W, H, spp, bounces, use_ao=False, ao=2.5, rng=RT_RNG_PHILOX, seed=1010, compat=1, cam=None,
+           aperture=(0.0, 0.0), focus=3.0):
+    if cam is None:
+        cam = readme_camera_oracle()
+    return tipe_rt.make_params(W, H, spp, bounces, cam, focus=focus, aperture=aperture, use_ao=use_ao, ao=ao,
+                               seed=seed, rng=rng, compat=compat)
+
+
+def oracle_render(bundle, p, row_hi=None, row_lo=0, nthreads=1, counters=False):
+    W, H = p.largeur_image, p.hauteur_image
+    if row_hi is None:
+        row_hi = H - 1
+    canva, alb, nrm, rad = (np.zeros((H, W, 3)) for _ in range(4))
+    cnt = oracle_ffi.counters() if counters else None
+    rc = oracle_ffi.oracle().oracle_render_rows(C.byref(bundle.scene), C.byref(p), row_hi, row_lo, nthreads, 1,
+                                                canva.ctypes.data, alb.ctypes.data, nrm.ctypes.data,
+                                                rad.ctypes.data, cnt)
+    assert rc == 0, rc
+    out = dict(canva=canva, albedo=alb, normal=nrm, radiance=rad)
+    if counters:
+        out["counters"] = np.array(list(cnt), dtype=np.uint64)
+    return out
+
+
+def ppm_md5(canva):
+    H, W, _ = canva.shape
+    lines = ["P3\n%d %d\n255\n" % (W, H)]
+    for j in range(H - 1, -1, -1):
+        row = canva[j].astype(np.int64)
+        lines.extend("%d %d %d\n" % (r, g, b) for r, g, b in row)
+    return hashlib.md5("".join(lines).encode()).hexdigest()
+
+
+def rmse_per_channel(a, b):
+    d = (np.asarray(a, dtype=np.float64) - np.asarray(b, dtype=np.float64)).reshape(-1, 3)
+    return np.sqrt((d * d).mean(axis=0))

@@ -1,0 +1,239 @@
+"""GPU parity: librt_hip.so (through the C-ABI) vs the CPU oracle in
+RT_RNG_PHILOX mode on identical seeded inputs.
+
+The kernel performs the reference's IEEE operations in the same order as the
+oracle, so the bar is BIT-EXACT equality of canva (8-bit resolve), albedo,
+normal and pre-gamma radiance.  north_star's tolerance (per-channel RMSE
+<= 1e-4 on float accumulation) is asserted as well, as the outer bound.
+"""
+import ctypes as C
+import threading
+
+import numpy as np
+import pytest
+
+import helpers
+import oracle_ffi
+import tipe_rt
+from tipe_rt.types import ThreadData, Sphere, Triangle, Material
+
+pytestmark = pytest.mark.gpu
+
+RMSE_TOL = 1e-4   # north_star: per-channel RMSE on identical seeds
+
+
+def gpu_render(bundle, p, tiling=None, radiance=True):
+    """Device path: rt_scene_upload + rt_render_async into torch buffers."""
+    import torch
+    W, H = p.largeur_image, p.hauteur_image
+    if tiling is None:
+        tiling = tipe_rt.band_tiling(0, H - 1)
+    rows = tiling.n_tiles * tiling.tile_rows
+    dev = torch.device("cuda:0")
+    bufs = [torch.full((rows, W, 3), -1.0, dtype=torch.float64, device=dev) for _ in range(4)]
+    ds = tipe_rt.DeviceScene(bundle.scene, 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    tipe_rt.render_async(ds, p, tiling, bufs[0].data_ptr(), bufs[1].data_ptr(), bufs[2].data_ptr(),
+                         bufs[3].data_ptr() if radiance else None, stream)
+    torch.cuda.synchronize()
+    ds.close()
+    return [b.cpu().numpy() for b in bufs]
+
+
+def assert_same(gpu, ref, what):
+    assert gpu.shape == ref.shape, what
+    diff = np.argwhere(gpu != ref)
+    if len(diff):
+        j, i, c = diff[0]
+        raise AssertionError("%s: %d mismatching values; first at row %d col %d ch %d: gpu %r oracle %r" %
+                             (what, len(diff), j, i, c, gpu[j, i, c], ref[j, i, c]))
+
+
+def check_parity(bundle, p):
+    ref = helpers.oracle_render(bundle, p)
+    canva, alb, nrm, rad = gpu_render(bundle, p)
+    assert (helpers.rmse_per_channel(rad, ref["radiance"]) <= RMSE_TOL).all()
+    assert (helpers.rmse_per_channel(canva / 255.0, ref["canva"] / 255.0) <= RMSE_TOL).all()
+    assert_same(canva, ref["canva"], "canva")
+    assert_same(rad, ref["radiance"], "radiance")
+    assert_same(alb, ref["albedo"], "albedo")
+    assert_same(nrm, ref["normal"], "normal")
+    return ref
+
+
+# ---- device primitives ------------------------------------------------------
+def test_device_math_bitexact():
+    o = oracle_ffi.oracle()
+    rng = np.random.default_rng(7)
+    n = 4096
+    k = rng.integers(0, 2 ** 31, n)
+    xs = np.concatenate([2.0 * (k / 2147483648.0) - 1.0, [-1.0, -0.5, 0.5, 0.0, 1e-20, -1e-300]])
+    got = tipe_rt.selftest_math(0, xs, len(xs))
+    want = np.array([o.oracle_pm_acos(x) for x in xs])
+    assert (got.view(np.uint64) == want.view(np.uint64)).all()
+    fs = np.concatenate([rng.uniform(0, 2 * np.pi, n), rng.uniform(0, np.pi, n), [0.0, np.pi / 2, 1e-30]])
+    fs = fs.astype(np.float32).astype(np.float64)
+    got = tipe_rt.selftest_math(1, fs, len(fs))
+    assert (got == np.array([o.oracle_pm_sinf(x) for x in fs])).all()
+    got = tipe_rt.selftest_math(2, fs, len(fs))
+    assert (got == np.array([o.oracle_pm_cosf(x) for x in fs])).all()
+    xy = np.stack([1.0 + rng.uniform(-1e-15, 1e-15, n), rng.choice([2.0, 2.5, 3.0, 8.0, 0.5], n)], 1).ravel()
+    got = tipe_rt.selftest_math(3, xy, n)
+    want = np.array([o.oracle_pm_pow(xy[2 * i], xy[2 * i + 1]) for i in range(n)])
+    assert (got.view(np.uint64) == want.view(np.uint64)).all()
+    xs = rng.uniform(0, 1e6, n) * rng.choice([1e-300, 1e-10, 1.0, 1e300], n)
+    assert (tipe_rt.selftest_math(4, xs, n).view(np.uint64) == np.sqrt(xs).view(np.uint64)).all()
+    ab = rng.uniform(-10, 10, 2 * n)
+    assert (tipe_rt.selftest_math(5, ab, n) == ab[0::2] / ab[1::2]).all()
+    fs = rng.uniform(0, 1e4, n).astype(np.float32)
+    assert (tipe_rt.selftest_math(6, fs.astype(np.float64), n) == np.sqrt(fs).astype(np.float64)).all()
+
+
+def test_device_philox_matches_oracle():
+    o = oracle_ffi.oracle()
+    rng = np.random.default_rng(3)
+    n = 512
+    q = rng.integers(0, 2 ** 32, (n, 6), dtype=np.uint64)
+    got = tipe_rt.selftest_math(7, q.astype(np.float64).ravel(), n).astype(np.uint64).reshape(n, 4)
+    for i in range(n):
+        ctr = (C.c_uint * 4)(*[int(x) for x in q[i, :4]])
+        key = (C.c_uint * 2)(*[int(x) for x in q[i, 4:]])
+        out = (C.c_uint * 4)()
+        o.oracle_philox(ctr, key, out)
+        assert list(out) == [int(x) for x in got[i]]
+
+
+# ---- full renders -------------------------------------------------------------
+def test_cornell_spheres_bitexact():
+    check_parity(helpers.cornell(), helpers.params(64, 48, 16, 5))
+
+
+def test_cornell_six_bounces_odd_size():
+    check_parity(helpers.cornell(), helpers.params(37, 29, 9, 6, seed=77))
+
+
+def test_cornell_ao_compat_int():
+    # AO_intensity 2.5 -> 2 (ThreadData int, main.c:43)
+    check_parity(helpers.cornell(), helpers.params(48, 36, 8, 8, use_ao=True, ao=2.5))
+
+
+def test_cornell_ao_fractional_intensity():
+    check_parity(helpers.cornell(), helpers.params(32, 24, 8, 6, use_ao=True, ao=2.5, compat=0))
+
+
+def test_depth_of_field_aperture():
+    check_parity(helpers.cornell(), helpers.params(40, 30, 8, 5, aperture=(0.3, 0.2), compat=0, focus=2.5))
+
+
+def test_pyramid_texture_refraction():
+    ref = check_parity(helpers.pyramid_scene(), helpers.params(64, 48, 16, 6))
+    cnt = helpers.oracle_render(helpers.pyramid_scene(), helpers.params(16, 12, 4, 6), counters=True)["counters"]
+    assert cnt[tipe_rt.types.RT_CNT_REFRACT] > 0 and cnt[tipe_rt.types.RT_CNT_TEX_HITS] > 0
+    assert ref["canva"].max() > 0
+
+
+def test_mineways_alpha_holes():
+    tris, qm, mats, tw, th, nm = tipe_rt.scenes.load_mesh_fixture("mineways")
+    for t in tris:
+        for P in (t.A, t.B, t.C):
+            P.e[0] = P.e[0] * 0.1 - 0.2
+            P.e[1] = P.e[1] * 0.1 - 1.0
+            P.e[2] = P.e[2] * 0.1 - 2.5
+    bundle = helpers.SceneBundle(tipe_rt.scenes.cornell_spheres(), (tris, qm, mats, tw, th, nm))
+    check_parity(bundle, helpers.params(40, 30, 4, 6))
+
+
+def test_counters_match_oracle():
+    import torch
+    bundle = helpers.pyramid_scene()
+    p = helpers.params(32, 24, 8, 6, use_ao=True)
+    ref = helpers.oracle_render(bundle, p, counters=True)["counters"]
+    ds = tipe_rt.DeviceScene(bundle.scene, 0)
+    d_cnt = torch.zeros(tipe_rt.RT_NCOUNTERS, dtype=torch.int64, device="cuda:0")
+    tipe_rt.count_async(ds, p, tipe_rt.band_tiling(0, 23), d_cnt.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = d_cnt.cpu().numpy().astype(np.uint64)
+    ds.close()
+    assert list(got) == list(ref), dict(zip(tipe_rt.COUNTER_NAMES, zip(got, ref)))
+
+
+# ---- boundary behaviour --------------------------------------------------------
+def test_render_rows_host_api_band():
+    bundle = helpers.cornell()
+    p = helpers.params(48, 36, 4, 5)
+    ref = helpers.oracle_render(bundle, p)
+    canva = np.full((36, 48, 3), -7.0)
+    alb = np.full((36, 48, 3), -7.0)
+    nrm = np.full((36, 48, 3), -7.0)
+    tipe_rt.check(tipe_rt.lib().rt_render_rows(C.byref(bundle.scene), C.byref(p), 20, 9, canva.ctypes.data,
+                                               alb.ctypes.data, nrm.ctypes.data))
+    assert (canva[9:21] == ref["canva"][9:21]).all()
+    assert (alb[9:21] == ref["albedo"][9:21]).all() and (nrm[9:21] == ref["normal"][9:21]).all()
+    untouched = np.ones(36, bool)
+    untouched[9:21] = False
+    assert (canva[untouched] == -7.0).all()       # only the named rows are written
+
+
+def test_cyclic_tiles_assemble_to_full_frame():
+    import torch
+    bundle = helpers.cornell()
+    W, H, k, world = 40, 30, 4, 3
+    p = helpers.params(W, H, 4, 5)
+    ref = helpers.oracle_render(bundle, p)
+    ds = tipe_rt.DeviceScene(bundle.scene, 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    per_rank = tipe_rt.cyclic_tiling(H, k, 0, world).n_tiles
+    gathered = torch.zeros((world, per_rank * k, W, 3), dtype=torch.float64, device="cuda:0")
+    for r in range(world):
+        t = tipe_rt.cyclic_tiling(H, k, r, world)
+        tipe_rt.render_async(ds, p, t, gathered[r].data_ptr(), stream=stream)
+    full = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda:0")
+    tipe_rt.assemble_async(gathered.data_ptr(), world, k, per_rank * k, W, H, full.data_ptr(), stream)
+    torch.cuda.synchronize()
+    ds.close()
+    assert (full.cpu().numpy() == ref["canva"]).all()
+
+
+def test_fill_canva_pthread_dropin():
+    """rt_fill_canva takes main.c's ThreadData; 4 threads on disjoint bands."""
+    bundle = helpers.cornell()
+    W, H = 40, 30
+    p = helpers.params(W, H, 4, 5)
+    ref = helpers.oracle_render(bundle, p)
+    canva, alb, nrm = (np.zeros((H, W, 3)) for _ in range(3))
+    tds = []
+    bands = [(29, 22), (21, 15), (14, 8), (7, 0)]
+    for hi, lo in bands:
+        td = ThreadData()
+        td.start_row, td.end_row = hi, lo
+        td.canva = C.cast(canva.ctypes.data, C.POINTER(tipe_rt.Vec3))
+        td.albedo_tab = C.cast(alb.ctypes.data, C.POINTER(tipe_rt.Vec3))
+        td.normal_tab = C.cast(nrm.ctypes.data, C.POINTER(tipe_rt.Vec3))
+        td.cam = p.cam
+        td.largeur_image, td.hauteur_image = W, H
+        td.nbRayonParPixel, td.nbRebondMax = 4, 5
+        td.total_pixels = W * H
+        td.sphere_list = C.cast(bundle.spheres, C.POINTER(Sphere))
+        td.nbSpheres = len(bundle.spheres)
+        td.focus_distance = 3
+        tds.append(td)
+    res = []
+    ths = [threading.Thread(target=lambda t=t: res.append(tipe_rt.lib().rt_fill_canva(C.byref(t)))) for t in tds]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert all(r is None for r in res), tipe_rt.lib().rt_last_error()
+    assert (canva == ref["canva"]).all() and (alb == ref["albedo"]).all() and (nrm == ref["normal"]).all()
+
+
+def test_invalid_arguments_fail_loudly():
+    bundle = helpers.cornell()
+    p = helpers.params(8, 6, 0, 5)
+    canva = np.zeros((6, 8, 3))
+    rc = tipe_rt.lib().rt_render_rows(C.byref(bundle.scene), C.byref(p), 5, 0, canva.ctypes.data, None, None)
+    assert rc == tipe_rt.RT_EINVAL and b"nbRayonParPixel" in tipe_rt.lib().rt_last_error()
+    p = helpers.params(8, 6, 1, 5, rng=tipe_rt.RT_RNG_GLIBC)
+    rc = tipe_rt.lib().rt_render_rows(C.byref(bundle.scene), C.byref(p), 5, 0, canva.ctypes.data, None, None)
+    assert rc == tipe_rt.RT_EUNSUPPORTED

@@ -1,0 +1,553 @@
+// rt_api.cpp — C-ABI of librt_hip.so (include/rt/rt.h): validation, scene
+// upload into the HBM layout of rt_internal.h, launch descriptors, the
+// host-buffer drop-ins (rt_render_rows / rt_fill_canva) and diagnostics.
+// Every HIP call is checked; failures return RT_E* and set rt_last_error().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rt/rt.h"
+#include "rt_internal.h"
+
+using namespace rt;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(RT_EDEVICE, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                                \
+    } while (0)
+
+std::mutex g_mu;
+std::vector<int> g_devices;
+bool g_inited = false;
+
+// Restores the caller's current device on scope exit (torch owns it in bench).
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(dev) == hipSuccess) ok = true;
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int validate_scene(const rt_scene* sc)
+{
+    if (!sc) return fail(RT_EINVAL, "scene is NULL");
+    if (sc->nbSpheres < 0 || sc->nbTriangles < 0) return fail(RT_EINVAL, "negative primitive count");
+    if (sc->nbSpheres > 0 && !sc->sphere_list) return fail(RT_EINVAL, "sphere_list is NULL");
+    if (sc->nbTriangles > 0) {
+        if (!sc->triangle_list || !sc->mat_list || !sc->quelMatPourTri)
+            return fail(RT_EINVAL, "triangles need triangle_list, mat_list and quelMatPourTri");
+        if (sc->tex_width < 1 || sc->tex_height < 1 || sc->nbMaterials < 1)
+            return fail(RT_EINVAL, "texture table %dx%d x %d materials", sc->tex_width, sc->tex_height,
+                        sc->nbMaterials);
+        for (int i = 0; i < sc->nbTriangles; ++i)
+            if (sc->quelMatPourTri[i] < 0 || sc->quelMatPourTri[i] >= sc->nbMaterials)
+                return fail(RT_EINVAL, "quelMatPourTri[%d] = %d outside [0, %d)", i, sc->quelMatPourTri[i],
+                            sc->nbMaterials);
+    }
+    return RT_OK;
+}
+
+int validate_params(const rt_params* p)
+{
+    if (!p) return fail(RT_EINVAL, "params is NULL");
+    if (p->largeur_image < 1 || p->hauteur_image < 1)
+        return fail(RT_EINVAL, "image %dx%d", p->largeur_image, p->hauteur_image);
+    if (p->nbRayonParPixel < 1) return fail(RT_EINVAL, "nbRayonParPixel %d < 1", p->nbRayonParPixel);
+    if (p->nbRebondMax < 0) return fail(RT_EINVAL, "nbRebondMax %d < 0", p->nbRebondMax);
+    if (p->rng == RT_RNG_GLIBC)
+        return fail(RT_EUNSUPPORTED,
+                    "RT_RNG_GLIBC is one sequential rand() stream with data-dependent draw counts; "
+                    "only the CPU oracle replays it");
+    if (p->rng != RT_RNG_PHILOX) return fail(RT_EINVAL, "unknown rng %d", p->rng);
+    if ((unsigned long long)p->largeur_image * (unsigned long long)p->hauteur_image > 0xffffffffull)
+        return fail(RT_EUNSUPPORTED, "pixel index exceeds the 32-bit Philox counter word");
+    return RT_OK;
+}
+
+int validate_tiling(const rt_tiling* t)
+{
+    if (!t) return fail(RT_EINVAL, "tiling is NULL");
+    if (t->tile_rows < 1 || t->tile_step < 1 || t->tile_first < 0 || t->n_tiles < 0 || t->row_base < 0)
+        return fail(RT_EINVAL, "bad tiling {%d,%d,%d,%d,%d}", t->row_base, t->tile_rows, t->tile_first,
+                    t->tile_step, t->n_tiles);
+    if ((long long)t->n_tiles * t->tile_rows > (1ll << 30)) return fail(RT_EINVAL, "tiling too large");
+    return RT_OK;
+}
+
+}  // namespace
+
+struct rt_device_scene {
+    int device = 0;
+    int ns = 0, nt = 0, tw = 1, th = 1;
+    long long n_texels = 0;
+    SphGeo* sph = nullptr;
+    DevMat* sph_mat = nullptr;
+    TriGeo* tri = nullptr;
+    TriTex* tri_tex = nullptr;
+    DevMat* texels = nullptr;
+};
+
+namespace {
+
+DevMat to_dev(const rt_material& m)
+{
+    return DevMat{m.diffuseColor.e[0],  m.diffuseColor.e[1],  m.diffuseColor.e[2], m.emissionColor.e[0],
+                  m.emissionColor.e[1], m.emissionColor.e[2], m.emissionStrength,  m.reflectionStrength,
+                  m.alpha,              m.materialIndex};
+}
+
+void free_scene(rt_device_scene* s)
+{
+    if (!s) return;
+    DeviceGuard g(s->device);
+    (void)hipFree(s->sph);
+    (void)hipFree(s->sph_mat);
+    (void)hipFree(s->tri);
+    (void)hipFree(s->tri_tex);
+    (void)hipFree(s->texels);
+    delete s;
+}
+
+template <class T>
+int upload(T** dst, const std::vector<T>& src)
+{
+    if (src.empty()) return RT_OK;
+    HIP_TRY(hipMalloc((void**)dst, src.size() * sizeof(T)));
+    HIP_TRY(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+int ensure_init_locked()
+{
+    if (g_inited) return RT_OK;
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (n < 1) return fail(RT_EDEVICE, "no HIP device");
+    g_devices.assign(1, 0);
+    g_inited = true;
+    return RT_OK;
+}
+
+int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling* t, KParams& kp)
+{
+    std::memset(&kp, 0, sizeof kp);
+    kp.sph = sc->sph;
+    kp.sph_mat = sc->sph_mat;
+    kp.tri = sc->tri;
+    kp.tri_tex = sc->tri_tex;
+    kp.texels = sc->texels;
+    kp.ns = sc->ns;
+    kp.nt = sc->nt;
+    kp.tw = sc->tw;
+    kp.th = sc->th;
+    kp.n_texels = sc->n_texels;
+    kp.W = p->largeur_image;
+    kp.H = p->hauteur_image;
+    kp.S = p->nbRayonParPixel;
+    kp.B = p->nbRebondMax;
+    for (int i = 0; i < 3; ++i) {
+        kp.cam_o[i] = p->cam.origin.e[i];
+        kp.cam_h[i] = p->cam.horizontal.e[i];
+        kp.cam_v[i] = p->cam.vertical.e[i];
+        kp.cam_c[i] = p->cam.coin_bas_gauche.e[i];
+    }
+    kp.focus = p->focus_distance;
+    kp.ox = p->ouverture_x;
+    kp.oy = p->ouverture_y;
+    kp.AO = p->AO_intensity;
+    if (p->compat_int_truncation) {     // ThreadData int fields, main.c:42-43
+        kp.focus = (double)(int)kp.focus;
+        kp.ox = (double)(int)kp.ox;
+        kp.oy = (double)(int)kp.oy;
+        kp.AO = (double)(int)kp.AO;
+    }
+    kp.useAO = p->useAO ? 1 : 0;
+    kp.key0 = (uint32_t)p->seed;
+    kp.key1 = (uint32_t)(p->seed >> 32);
+    kp.row_base = t->row_base;
+    kp.tile_rows = t->tile_rows;
+    kp.tile_first = t->tile_first;
+    kp.tile_step = t->tile_step;
+    kp.n_tiles = t->n_tiles;
+    kp.row_end = p->hauteur_image;
+    kp.local_rows = t->n_tiles * t->tile_rows;
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void rt_params_init(rt_params* p)
+{
+    if (!p) return;
+    std::memset(p, 0, sizeof *p);
+    p->rng = RT_RNG_PHILOX;
+    p->seed = 1010ull;
+    p->compat_int_truncation = 1;
+}
+
+int rt_init(int ndev, const int* devices)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (n < 1) return fail(RT_EDEVICE, "no HIP device");
+    g_devices.clear();
+    if (ndev <= 0 || !devices) {
+        g_devices.push_back(0);
+    } else {
+        for (int i = 0; i < ndev; ++i) {
+            if (devices[i] < 0 || devices[i] >= n) return fail(RT_EINVAL, "device %d of %d", devices[i], n);
+            g_devices.push_back(devices[i]);
+        }
+    }
+    g_inited = true;
+    return RT_OK;
+}
+
+void rt_shutdown(void)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_devices.clear();
+    g_inited = false;
+}
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+const char* rt_version(void) { return "tipe-raytracer-mi355x 0.1 (abi 1, gfx950, fp64 exact)"; }
+
+int rt_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
+{
+    if (!out) return fail(RT_EINVAL, "out is NULL");
+    *out = nullptr;
+    int rc = validate_scene(scene);
+    if (rc) return rc;
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(RT_EINVAL, "device %d of %d", device, n);
+    DeviceGuard guard(device);
+    if (!guard.ok) return fail(RT_EDEVICE, "hipSetDevice(%d) failed", device);
+
+    std::vector<SphGeo> sph((size_t)scene->nbSpheres);
+    std::vector<DevMat> sph_mat((size_t)scene->nbSpheres);
+    for (int i = 0; i < scene->nbSpheres; ++i) {
+        const rt_sphere& s = scene->sphere_list[i];
+        sph[i] = SphGeo{s.center.e[0], s.center.e[1], s.center.e[2], s.radius * s.radius};
+        sph_mat[i] = to_dev(s.mat);
+    }
+    std::vector<TriGeo> tri((size_t)scene->nbTriangles);
+    std::vector<TriTex> tex((size_t)scene->nbTriangles);
+    for (int i = 0; i < scene->nbTriangles; ++i) {
+        const rt_triangle& t = scene->triangle_list[i];
+        const double abx = t.B.e[0] - t.A.e[0], aby = t.B.e[1] - t.A.e[1], abz = t.B.e[2] - t.A.e[2];
+        const double acx = t.C.e[0] - t.A.e[0], acy = t.C.e[1] - t.A.e[1], acz = t.C.e[2] - t.A.e[2];
+        TriGeo& g = tri[i];
+        g.ax = t.A.e[0];
+        g.ay = t.A.e[1];
+        g.az = t.A.e[2];
+        g.abx = abx;
+        g.aby = aby;
+        g.abz = abz;
+        g.acx = acx;
+        g.acy = acy;
+        g.acz = acz;
+        g.nx = aby * acz - abz * acy;          // vec3_cross, vec3.h:121-127
+        g.ny = abz * acx - abx * acz;
+        g.nz = abx * acy - aby * acx;
+        TriTex& x = tex[i];
+        x.bx = t.B.e[0];
+        x.by = t.B.e[1];
+        x.bz = t.B.e[2];
+        x.cx = t.C.e[0];
+        x.cy = t.C.e[1];
+        x.cz = t.C.e[2];
+        x.uau = t.uvA.u;
+        x.uav = t.uvA.v;
+        x.ubu = t.uvB.u;
+        x.ubv = t.uvB.v;
+        x.ucu = t.uvC.u;
+        x.ucv = t.uvC.v;
+        x.mat = scene->quelMatPourTri[i];
+        x.pad = 0;
+    }
+    std::vector<DevMat> texels;
+    long long n_texels = 0;
+    if (scene->nbTriangles > 0) {
+        n_texels = (long long)scene->nbMaterials * scene->tex_width * scene->tex_height;
+        texels.resize((size_t)n_texels);
+        for (long long i = 0; i < n_texels; ++i) texels[(size_t)i] = to_dev(scene->mat_list[i]);
+    }
+
+    rt_device_scene* ds = new rt_device_scene();
+    ds->device = device;
+    ds->ns = scene->nbSpheres;
+    ds->nt = scene->nbTriangles;
+    ds->tw = scene->nbTriangles > 0 ? scene->tex_width : 1;
+    ds->th = scene->nbTriangles > 0 ? scene->tex_height : 1;
+    ds->n_texels = n_texels;
+    if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
+        (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels))) {
+        free_scene(ds);
+        return rc;
+    }
+    *out = ds;
+    return RT_OK;
+}
+
+void rt_scene_release(rt_device_scene* scene) { free_scene(scene); }
+
+int rt_render_async(const rt_device_scene* scene, const rt_params* params, const rt_tiling* tiling,
+                    const rt_frame* frame, void* hip_stream)
+{
+    if (!scene) return fail(RT_EINVAL, "scene is NULL");
+    int rc;
+    if ((rc = validate_params(params)) || (rc = validate_tiling(tiling))) return rc;
+    if (!frame || !frame->canva) return fail(RT_EINVAL, "frame.canva is NULL");
+    KParams kp;
+    make_kparams(scene, params, tiling, kp);
+    kp.canva = (double*)frame->canva;
+    kp.albedo = (double*)frame->albedo;
+    kp.normal = (double*)frame->normal;
+    kp.radiance = (double*)frame->radiance;
+    if (kp.local_rows == 0 || kp.W == 0) return RT_OK;
+    DeviceGuard guard(scene->device);
+    const int e = launch_render(kp, hip_stream);
+    if (e) return fail(RT_EDEVICE, "render launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+int rt_count_async(const rt_device_scene* scene, const rt_params* params, const rt_tiling* tiling,
+                   unsigned long long* d_counters, void* hip_stream)
+{
+    if (!scene) return fail(RT_EINVAL, "scene is NULL");
+    int rc;
+    if ((rc = validate_params(params)) || (rc = validate_tiling(tiling))) return rc;
+    if (!d_counters) return fail(RT_EINVAL, "d_counters is NULL");
+    KParams kp;
+    make_kparams(scene, params, tiling, kp);
+    kp.counters = d_counters;
+    if (kp.local_rows == 0) return RT_OK;
+    DeviceGuard guard(scene->device);
+    const int e = launch_count(kp, hip_stream);
+    if (e) return fail(RT_EDEVICE, "count launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+int rt_assemble_async(const rt_color* gathered, int world, int tile_rows, int rows_per_rank, int W, int H,
+                      rt_color* out, void* hip_stream)
+{
+    if (!gathered || !out) return fail(RT_EINVAL, "NULL buffer");
+    if (world < 1 || tile_rows < 1 || rows_per_rank < 0 || W < 1 || H < 1 || rows_per_rank % tile_rows)
+        return fail(RT_EINVAL, "bad assemble geometry");
+    const long long tiles = (H + tile_rows - 1) / tile_rows;
+    if ((long long)world * (rows_per_rank / tile_rows) < tiles)
+        return fail(RT_EINVAL, "gather holds %d tiles/rank x %d ranks < %lld tiles", rows_per_rank / tile_rows,
+                    world, tiles);
+    const int e = launch_assemble((const double*)gathered, world, tile_rows, rows_per_rank, W, H, (double*)out,
+                                  hip_stream);
+    if (e) return fail(RT_EDEVICE, "assemble launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, int row_lo, rt_color* canva,
+                   rt_color* albedo, rt_color* normal)
+{
+    int rc;
+    if ((rc = validate_scene(scene)) || (rc = validate_params(params))) return rc;
+    if (!canva) return fail(RT_EINVAL, "canva is NULL");
+    if (row_lo < 0 || row_hi >= params->hauteur_image || row_hi < row_lo)
+        return fail(RT_EINVAL, "rows %d..%d outside [0, %d)", row_hi, row_lo, params->hauteur_image);
+    std::vector<int> devs;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if ((rc = ensure_init_locked())) return rc;
+        devs = g_devices;
+    }
+    const int W = params->largeur_image;
+    const int nrows = row_hi - row_lo + 1;
+    const int ndev = (int)devs.size();
+    // One device: one band.  Several: cyclic 8-row tiles (load balance).
+    const int k = ndev == 1 ? nrows : 8;
+    const int ntiles = (nrows + k - 1) / k;
+
+    struct Slot {
+        rt_device_scene* sc = nullptr;
+        hipStream_t st = nullptr;
+        double* buf = nullptr;      // canva | albedo | normal planes
+        int n_tiles = 0;
+        size_t plane = 0;
+    };
+    std::vector<Slot> slots((size_t)ndev);
+    auto cleanup = [&]() {
+        for (auto& s : slots) {
+            if (s.sc) {
+                DeviceGuard g(s.sc->device);
+                if (s.st) (void)hipStreamSynchronize(s.st);
+                (void)hipFree(s.buf);
+                if (s.st) (void)hipStreamDestroy(s.st);
+            }
+            rt_scene_release(s.sc);
+        }
+    };
+    for (int q = 0; q < ndev; ++q) {
+        Slot& s = slots[(size_t)q];
+        s.n_tiles = ntiles > q ? (ntiles - q + ndev - 1) / ndev : 0;
+        if (s.n_tiles == 0) continue;
+        if ((rc = rt_scene_upload(devs[(size_t)q], scene, &s.sc))) {
+            cleanup();
+            return rc;
+        }
+        DeviceGuard g(devs[(size_t)q]);
+        s.plane = (size_t)s.n_tiles * k * W * 3;
+        hipError_t e = hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMalloc((void**)&s.buf, s.plane * 3 * sizeof(double));
+        if (e != hipSuccess) {
+            cleanup();
+            return fail(RT_EDEVICE, "device %d setup: %s", devs[(size_t)q], hipGetErrorString(e));
+        }
+        rt_tiling t{row_lo, k, q, ndev, s.n_tiles};
+        KParams kp;
+        make_kparams(s.sc, params, &t, kp);
+        kp.row_end = row_hi + 1;
+        kp.canva = s.buf;
+        kp.albedo = albedo ? s.buf + s.plane : nullptr;
+        kp.normal = normal ? s.buf + 2 * s.plane : nullptr;
+        const int le = launch_render(kp, s.st);
+        if (le) {
+            cleanup();
+            return fail(RT_EDEVICE, "render launch: %s", hipGetErrorString((hipError_t)le));
+        }
+    }
+    std::vector<double> host;
+    for (int q = 0; q < ndev; ++q) {
+        Slot& s = slots[(size_t)q];
+        if (s.n_tiles == 0) continue;
+        DeviceGuard g(devs[(size_t)q]);
+        host.resize(s.plane * 3);
+        hipError_t e = hipMemcpyAsync(host.data(), s.buf, s.plane * 3 * sizeof(double), hipMemcpyDeviceToHost, s.st);
+        if (e == hipSuccess) e = hipStreamSynchronize(s.st);
+        if (e != hipSuccess) {
+            cleanup();
+            return fail(RT_EDEVICE, "device %d render/copy: %s", devs[(size_t)q], hipGetErrorString(e));
+        }
+        rt_color* outs[3] = {canva, albedo, normal};
+        for (int lt = 0; lt < s.n_tiles; ++lt) {
+            const int t = q + lt * ndev;
+            for (int y = 0; y < k; ++y) {
+                const int gr = row_lo + t * k + y;
+                if (gr > row_hi) break;
+                const size_t src = ((size_t)lt * k + y) * W * 3;
+                for (int p = 0; p < 3; ++p)
+                    if (outs[p])
+                        std::memcpy(outs[p] + (size_t)gr * W, host.data() + p * s.plane + src, sizeof(double) * 3 * W);
+            }
+        }
+    }
+    cleanup();
+    return RT_OK;
+}
+
+void* rt_fill_canva(void* arg)
+{
+    const rt_thread_data* d = (const rt_thread_data*)arg;
+    if (!d) {
+        fail(RT_EINVAL, "thread data is NULL");
+        return (void*)1;
+    }
+    int nmat = 0;
+    for (int i = 0; i < d->nbTriangles; ++i)
+        if (d->quelMatPourTri && d->quelMatPourTri[i] + 1 > nmat) nmat = d->quelMatPourTri[i] + 1;
+    rt_scene sc;
+    sc.sphere_list = d->sphere_list;
+    sc.nbSpheres = d->nbSpheres;
+    sc.triangle_list = d->triangle_list;
+    sc.nbTriangles = d->nbTriangles;
+    sc.mat_list = d->mat_list;
+    sc.tex_width = d->tex_width;
+    sc.tex_height = d->tex_height;
+    sc.nbMaterials = nmat;
+    sc.quelMatPourTri = d->quelMatPourTri;
+    rt_params p;
+    rt_params_init(&p);
+    p.largeur_image = d->largeur_image;
+    p.hauteur_image = d->hauteur_image;
+    p.nbRayonParPixel = d->nbRayonParPixel;
+    p.nbRebondMax = d->nbRebondMax;
+    p.cam = d->cam;
+    p.focus_distance = d->focus_distance;     // already int in ThreadData
+    p.ouverture_x = d->ouverture_x;
+    p.ouverture_y = d->ouverture_y;
+    p.AO_intensity = d->AO_intensity;
+    p.useAO = d->useAO ? 1 : 0;
+    p.compat_int_truncation = 0;
+    const int rc = rt_render_rows(&sc, &p, d->start_row, d->end_row, d->canva, d->albedo_tab, d->normal_tab);
+    return rc == RT_OK ? nullptr : (void*)1;
+}
+
+int rt_selftest_math(int op, const double* in, double* out, int n)
+{
+    if (!in || !out || n < 0 || op < 0 || op > 7) return fail(RT_EINVAL, "bad selftest arguments");
+    if (n == 0) return RT_OK;
+    int dev = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        int rc = ensure_init_locked();
+        if (rc) return rc;
+        dev = g_devices[0];
+    }
+    DeviceGuard guard(dev);
+    const size_t nin = (size_t)n * (op == 7 ? 6 : (op == 3 || op == 5) ? 2 : 1);
+    const size_t nout = (size_t)n * (op == 7 ? 4 : 1);
+    double *d_in = nullptr, *d_out = nullptr;
+    HIP_TRY(hipMalloc((void**)&d_in, nin * sizeof(double)));
+    hipError_t e = hipMalloc((void**)&d_out, nout * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpy(d_in, in, nin * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = (hipError_t)launch_selftest(op, d_in, d_out, n, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, nout * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    if (e != hipSuccess) return fail(RT_EDEVICE, "selftest: %s", hipGetErrorString(e));
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,185 @@
+// rt_device_math.h — device primitives of the RT_RNG_PHILOX stream spec:
+// the Philox4x32-10 stream and the portable transcendentals (DESIGN.md
+// "Portable math").  Built only from IEEE-754 +,-,*,/,sqrt, rint and bit
+// casts, compiled with -ffp-contract=off, so results are bit-identical to the
+// CPU restatement in oracle/pm_math.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace rt {
+
+// ---- Philox4x32-10 (Random123 / rocrand_philox4x32_10 engine) -------------
+struct Philox {
+    uint32_t w0, w1, w2, w3;
+};
+
+__device__ __forceinline__ Philox philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                uint32_t k0, uint32_t k1)
+{
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return Philox{c0, c1, c2, c3};
+}
+
+// Draw stream of one (pixel, sample): draw n = word (n & 3) of
+// philox(ctr = {n >> 2, 0, pixel, sample}, key = seed) >> 1   (rt.h)
+struct Stream {
+    uint32_t k0, k1, pixel, sample, n;
+    Philox blk;
+
+    __device__ __forceinline__ void start(uint32_t px, uint32_t s, uint32_t key0, uint32_t key1)
+    {
+        k0 = key0; k1 = key1; pixel = px; sample = s; n = 0;
+    }
+    __device__ __forceinline__ uint32_t next31()
+    {
+        const uint32_t slot = n & 3u;
+        if (slot == 0u) blk = philox4x32_10(n >> 2, 0u, pixel, sample, k0, k1);
+        const uint32_t w = slot == 0u ? blk.w0 : slot == 1u ? blk.w1 : slot == 2u ? blk.w2 : blk.w3;
+        ++n;
+        return w >> 1;
+    }
+};
+
+// rand()/(RAND_MAX + 1.0), rtutility.h:192
+__device__ __forceinline__ double unit31(uint32_t r) { return (double)r / 2147483648.0; }
+
+// ---- sin / cos of a float, evaluated in double, rounded to float ----------
+__device__ __forceinline__ int pm_sincos(float x, double& s, double& c)
+{
+    const double xd = (double)x;
+    const double kd = rint(xd * 0x1.45f306dc9c883p-1);
+    const double r = ((xd - kd * 0x1.921fb54400000p+0) - kd * 0x1.0b4611a600000p-34) - kd * 0x1.3198a2e000000p-69;
+    const double z = r * r;
+    const double ps = -0x1.5555555555555p-3 + z * (0x1.1111111111111p-7 + z * (-0x1.a01a01a01a01ap-13 +
+                      z * (0x1.71de3a556c734p-19 + z * (-0x1.ae64567f544e4p-26 + z * (0x1.6124613a86d09p-33 +
+                      z * (-0x1.ae7f3e733b81fp-41 + z * 0x1.952c77030ad4ap-49))))));
+    const double pc = -0x1.0000000000000p-1 + z * (0x1.5555555555555p-5 + z * (-0x1.6c16c16c16c17p-10 +
+                      z * (0x1.a01a01a01a01ap-16 + z * (-0x1.27e4fb7789f5cp-22 + z * (0x1.1eed8eff8d898p-29 +
+                      z * (-0x1.93974a8c07c9dp-37 + z * 0x1.ae7f3e733b81fp-45))))));
+    s = r + (r * z) * ps;
+    c = 1.0 + z * pc;
+    return (int)((long long)kd & 3);
+}
+
+__device__ __forceinline__ void pm_sincosf(float x, float& sn, float& cs)
+{
+    double s, c;
+    const int q = pm_sincos(x, s, c);
+    const double vs = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
+    const double vc = (q == 0) ? c : (q == 1) ? -s : (q == 2) ? -c : s;
+    sn = (float)vs;
+    cs = (float)vc;
+}
+
+// ---- acos (fdlibm scheme) --------------------------------------------------
+__device__ __forceinline__ double pm_acos_R(double z)
+{
+    const double p = z * (0x1.5555555555555p-3 + z * (-0x1.4d61203eb6f7dp-2 + z * (0x1.9c1550e884455p-3 +
+                     z * (-0x1.48228b5688f3bp-5 + z * (0x1.9efe07501b288p-11 + z * 0x1.23de10dfdf709p-15)))));
+    const double q = 1.0 + z * (-0x1.33a271c8a2d4bp+1 + z * (0x1.02ae59c598ac8p+1 +
+                     z * (-0x1.6066c1b8d0159p-1 + z * 0x1.3b8c5b12e9282p-4)));
+    return p / q;
+}
+
+__device__ __forceinline__ double pm_acos(double x)
+{
+    constexpr double PIO2_HI = 0x1.921fb54442d18p+0, PIO2_LO = 0x1.1a62633145c07p-54, PI = 0x1.921fb54442d18p+1;
+    const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+    const uint32_t hx = (uint32_t)(u >> 32);
+    const uint32_t ix = hx & 0x7fffffffu;
+    if (ix >= 0x3ff00000u) {
+        if (((ix - 0x3ff00000u) | (uint32_t)u) == 0u) return (hx >> 31) ? PI + 2.0 * PIO2_LO : 0.0;
+        return (x - x) / (x - x);
+    }
+    if (ix < 0x3fe00000u) {
+        if (ix <= 0x3c600000u) return PIO2_HI + PIO2_LO;
+        const double r = pm_acos_R(x * x);
+        return PIO2_HI - (x - (PIO2_LO - x * r));
+    }
+    if (hx >> 31) {
+        const double z = (1.0 + x) * 0.5;
+        const double r = pm_acos_R(z);
+        const double s = sqrt(z);
+        const double w = r * s - PIO2_LO;
+        return PI - 2.0 * (s + w);
+    }
+    const double z = (1.0 - x) * 0.5;
+    const double s = sqrt(z);
+    const double df = __longlong_as_double((long long)((unsigned long long)__double_as_longlong(s) & 0xffffffff00000000ull));
+    const double c = (z - df * df) / (s + df);
+    const double r = pm_acos_R(z);
+    const double w = r * s + c;
+    return 2.0 * (df + w);
+}
+
+// ---- pow ---------------------------------------------------------------------
+__device__ __forceinline__ double pm_from_bits(unsigned long long b) { return __longlong_as_double((long long)b); }
+
+__device__ __forceinline__ double pm_log(double x)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+    int e = (int)((u >> 52) & 0x7ff) - 1023;
+    double m = pm_from_bits((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+    if (m > 0x1.6a09e667f3bcdp+0) { m = m * 0.5; e = e + 1; }
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double t = 0x1.5555555555555p-2 + z * (0x1.999999999999ap-3 + z * (0x1.2492492492492p-3 +
+                     z * (0x1.c71c71c71c71cp-4 + z * (0x1.745d1745d1746p-4 + z * (0x1.3b13b13b13b14p-4 +
+                     z * (0x1.1111111111111p-4 + z * (0x1.e1e1e1e1e1e1ep-5 + z * (0x1.af286bca1af28p-5 +
+                     z * (0x1.8618618618618p-5 + z * 0x1.642c8590b2164p-5)))))))));
+    const double lm = 2.0 * s + (2.0 * s) * (z * t);
+    const double ed = (double)e;
+    return ed * 0x1.62e42fee00000p-1 + (lm + ed * 0x1.a39ef35793c76p-33);
+}
+
+__device__ __forceinline__ double pm_exp(double t)
+{
+    if (t > 709.0) return __longlong_as_double(0x7ff0000000000000ll);
+    if (t < -708.0) return 0.0;
+    const double kd = rint(t * 0x1.71547652b82fep+0);
+    const double r = (t - kd * 0x1.62e42fee00000p-1) - kd * 0x1.a39ef35793c76p-33;
+    const double p = 1.0 + r * (1.0 + r * (0x1.0000000000000p-1 + r * (0x1.5555555555555p-3 +
+                     r * (0x1.5555555555555p-5 + r * (0x1.1111111111111p-7 + r * (0x1.6c16c16c16c17p-10 +
+                     r * (0x1.a01a01a01a01ap-13 + r * (0x1.a01a01a01a01ap-16 + r * (0x1.71de3a556c734p-19 +
+                     r * (0x1.27e4fb7789f5cp-22 + r * (0x1.ae64567f544e4p-26 + r * (0x1.1eed8eff8d898p-29 +
+                     r * 0x1.6124613a86d09p-33))))))))))));
+    const int k = (int)kd;
+    const int k1 = k / 2, k2 = k - k1;
+    const double s1 = pm_from_bits((unsigned long long)(k1 + 1023) << 52);
+    const double s2 = pm_from_bits((unsigned long long)(k2 + 1023) << 52);
+    return (p * s1) * s2;
+}
+
+__device__ __forceinline__ double pm_pow(double x, double y)
+{
+    if (y == 0.0) return 1.0;
+    if (y == (double)(int)y && y <= 64.0 && y >= -64.0) {
+        const int n = (int)y;
+        unsigned un = (unsigned)(n < 0 ? -n : n);
+        double res = 1.0, base = x;
+        while (un) {
+            if (un & 1u) res = res * base;
+            base = base * base;
+            un >>= 1;
+        }
+        return n < 0 ? 1.0 / res : res;
+    }
+    const double inf = __longlong_as_double(0x7ff0000000000000ll);
+    if (x != x || y != y) return x + y;
+    if (x == 0.0) return y > 0.0 ? 0.0 : inf;
+    if (x < 0.0) return (x - x) / (x - x);
+    if (x == inf) return y > 0.0 ? inf : 0.0;
+    if (x < 0x1p-1022) return pm_exp(y * (pm_log(x * 0x1p54) - 54.0 * 0x1.62e42fefa39efp-1));
+    return pm_exp(y * pm_log(x));
+}
+
+}  // namespace rt

@@ -1,0 +1,73 @@
+// rt_internal.h — device-side scene layout and launch descriptors shared by
+// the C-ABI (rt_api.cpp) and the kernels (rt_kernels.hip).
+//
+// HBM layout of one uploaded scene (DESIGN.md "Data layout"):
+//   SphGeo  [ns]  32 B   center, radius^2      — read wave-uniformly (SMEM)
+//   DevMat  [ns]  80 B   sphere material       — gathered for the winner only
+//   TriGeo  [nt]  96 B   A, B-A, C-A, N        — read wave-uniformly (SMEM)
+//   TriTex  [nt]  112 B  B, C, uvA/B/C, mat    — gathered for the winner only
+//   DevMat  [nm*th*tw]   texel table (reference `material` records)
+#pragma once
+#include <cstdint>
+
+namespace rt {
+
+struct SphGeo { double cx, cy, cz, r2; };            // r2 = radius*radius (sphere.h:22)
+struct DevMat {                                       // == material, hitinfo.h:6-13
+    double dr, dg, db;       // diffuseColor
+    double er, eg, eb;       // emissionColor
+    double es, rs, alpha, ior;
+};
+struct TriGeo {                                       // mesh.h:72-74 precomputed
+    double ax, ay, az;
+    double abx, aby, abz;
+    double acx, acy, acz;
+    double nx, ny, nz;       // cross(B-A, C-A), unnormalised
+};
+struct TriTex {                                       // what tri_uvmapping reads
+    double bx, by, bz, cx, cy, cz;
+    double uau, uav, ubu, ubv, ucu, ucv;
+    int mat;                 // quelMatPourTri[i]
+    int pad;
+};
+static_assert(sizeof(SphGeo) == 32, "SphGeo");
+static_assert(sizeof(DevMat) == 80, "DevMat");
+static_assert(sizeof(TriGeo) == 96, "TriGeo");
+static_assert(sizeof(TriTex) == 104, "TriTex");
+
+// Everything one render launch needs, passed by value as the kernel argument.
+struct KParams {
+    // scene
+    const SphGeo* sph;
+    const DevMat* sph_mat;
+    const TriGeo* tri;
+    const TriTex* tri_tex;
+    const DevMat* texels;
+    int ns, nt;
+    int tw, th;
+    long long n_texels;
+    // image / integrator
+    int W, H, S, B;
+    double cam_o[3], cam_h[3], cam_v[3], cam_c[3];
+    double focus, ox, oy, AO;
+    int useAO;
+    uint32_t key0, key1;
+    // tiling
+    int row_base, tile_rows, tile_first, tile_step, n_tiles, row_end;
+    int local_rows;          // n_tiles * tile_rows
+    // outputs (device, local frame of local_rows x W colors)
+    double* canva;
+    double* albedo;
+    double* normal;
+    double* radiance;
+    unsigned long long* counters;
+};
+
+// launchers (rt_kernels.hip)
+int launch_render(const KParams& kp, void* stream);
+int launch_count(const KParams& kp, void* stream);
+int launch_assemble(const double* gathered, int world, int tile_rows, int rows_per_rank,
+                    int W, int H, double* out, void* stream);
+int launch_selftest(int op, const double* d_in, double* d_out, int n, void* stream);
+
+}  // namespace rt

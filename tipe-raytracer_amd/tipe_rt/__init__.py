@@ -1,0 +1,184 @@
+"""tipe_rt — Python mirror of the C-ABI in include/rt/rt.h (librt_hip.so).
+
+Thin ctypes plumbing for tests and bench.py; the product is the C-ABI
+library.  Loading fails loudly when librt_hip.so is missing: there is no CPU
+fallback on the product path.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from .types import (Vec3, Ray, Material, Sphere, UV, Triangle, Camera, ThreadData, Scene,  # noqa: F401
+                    Params, Tiling, Frame, RT_OK, RT_EINVAL, RT_EDEVICE, RT_ENOMEM, RT_EUNSUPPORTED,
+                    RT_RNG_PHILOX, RT_RNG_GLIBC, RT_NCOUNTERS, COUNTER_NAMES)
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
+HOST_LIB_PATH = os.path.join(PKG_DIR, "librt_host.so")
+
+
+class RTError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("rt error %d: %s" % (code, msg))
+        self.code = code
+
+
+_lib = None
+_host = None
+
+
+def lib():
+    """librt_hip.so with prototypes.  Raises if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError("librt_hip.so not built (%s): run `make -C tipe-raytracer_amd` "
+                               "or __graft_entry__.build(); there is no CPU fallback" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        P = C.POINTER
+        L.rt_params_init.argtypes = [P(Params)]
+        L.rt_init.argtypes = [C.c_int, P(C.c_int)]
+        L.rt_last_error.restype = C.c_char_p
+        L.rt_version.restype = C.c_char_p
+        L.rt_render_rows.argtypes = [P(Scene), P(Params), C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.rt_fill_canva.argtypes = [C.c_void_p]
+        L.rt_fill_canva.restype = C.c_void_p
+        L.rt_scene_upload.argtypes = [C.c_int, P(Scene), P(C.c_void_p)]
+        L.rt_scene_release.argtypes = [C.c_void_p]
+        L.rt_render_async.argtypes = [C.c_void_p, P(Params), P(Tiling), P(Frame), C.c_void_p]
+        L.rt_count_async.argtypes = [C.c_void_p, P(Params), P(Tiling), C.c_void_p, C.c_void_p]
+        L.rt_assemble_async.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                        C.c_void_p]
+        L.rt_selftest_math.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        _lib = L
+    return _lib
+
+
+EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error", "rt_version",
+                    "rt_device_count", "rt_render_rows", "rt_fill_canva", "rt_scene_upload",
+                    "rt_scene_release", "rt_render_async", "rt_assemble_async", "rt_count_async",
+                    "rt_selftest_math"]
+
+
+def check(rc):
+    if rc != RT_OK:
+        raise RTError(rc, lib().rt_last_error().decode())
+    return rc
+
+
+def host():
+    """librt_host.so (C host library: camera, OBJ/MTL/PPM IO)."""
+    global _host
+    if _host is None:
+        if not os.path.exists(HOST_LIB_PATH):
+            raise RuntimeError("librt_host.so not built (%s)" % HOST_LIB_PATH)
+        H = C.CDLL(HOST_LIB_PATH)
+        H.rt_host_init_camera.argtypes = [Vec3, Vec3, Vec3, C.c_double, C.c_double]
+        H.rt_host_init_camera.restype = Camera
+        _host = H
+    return _host
+
+
+def init_camera(origin, target, up, vfov, ratio):
+    """init_camera (camera.h:21-40) via the C host library."""
+    return host().rt_host_init_camera(Vec3(*origin), Vec3(*target), Vec3(*up), float(vfov), float(ratio))
+
+
+def make_scene(spheres=None, triangles=None, quel_mat=None, mat_list=None, tex_width=0, tex_height=0,
+               n_materials=0):
+    sc = Scene()
+    keep = []
+    if spheres is not None and len(spheres):
+        sc.sphere_list = C.cast(spheres, C.POINTER(Sphere))
+        sc.nbSpheres = len(spheres)
+        keep.append(spheres)
+    if triangles is not None and len(triangles):
+        sc.triangle_list = C.cast(triangles, C.POINTER(Triangle))
+        sc.nbTriangles = len(triangles)
+        sc.quelMatPourTri = C.cast(quel_mat, C.POINTER(C.c_int))
+        sc.mat_list = C.cast(mat_list, C.POINTER(Material))
+        sc.tex_width, sc.tex_height, sc.nbMaterials = tex_width, tex_height, n_materials
+        keep += [triangles, quel_mat, mat_list]
+    sc._keep = keep
+    return sc
+
+
+def make_params(W, H, spp, bounces, cam, focus=3.0, aperture=(0.0, 0.0), use_ao=False, ao=2.5,
+                seed=1010, rng=RT_RNG_PHILOX, compat=1):
+    p = Params()
+    p.largeur_image, p.hauteur_image = W, H
+    p.nbRayonParPixel, p.nbRebondMax = spp, bounces
+    p.cam = cam
+    p.focus_distance = focus
+    p.ouverture_x, p.ouverture_y = aperture
+    p.useAO, p.AO_intensity = int(bool(use_ao)), ao
+    p.compat_int_truncation = compat
+    p.rng, p.seed = rng, seed
+    return p
+
+
+def render_rows(scene, params, row_hi=None, row_lo=0, albedo=True, normal=True):
+    """rt_render_rows into fresh (H, W, 3) float64 arrays (canva, albedo, normal)."""
+    W, H = params.largeur_image, params.hauteur_image
+    if row_hi is None:
+        row_hi = H - 1
+    canva = np.zeros((H, W, 3))
+    alb = np.zeros((H, W, 3)) if albedo else None
+    nrm = np.zeros((H, W, 3)) if normal else None
+    check(lib().rt_render_rows(C.byref(scene), C.byref(params), row_hi, row_lo, canva.ctypes.data,
+                               alb.ctypes.data if alb is not None else None,
+                               nrm.ctypes.data if nrm is not None else None))
+    return canva, alb, nrm
+
+
+class DeviceScene:
+    """rt_scene_upload handle (released on close / garbage collection)."""
+
+    def __init__(self, scene, device=0):
+        self.handle = C.c_void_p()
+        check(lib().rt_scene_upload(device, C.byref(scene), C.byref(self.handle)))
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            lib().rt_scene_release(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def cyclic_tiling(H, tile_rows, rank, world):
+    """Rank `rank` of `world` with cyclic `tile_rows`-row tiles (rt.h rt_tiling)."""
+    n_tiles_total = (H + tile_rows - 1) // tile_rows
+    per_rank = (n_tiles_total + world - 1) // world
+    return Tiling(0, tile_rows, rank, world, per_rank)
+
+
+def band_tiling(row_lo, row_hi):
+    return Tiling(row_lo, row_hi - row_lo + 1, 0, 1, 1)
+
+
+def render_async(dscene, params, tiling, canva_ptr, albedo_ptr=None, normal_ptr=None, radiance_ptr=None,
+                 stream=None):
+    fr = Frame(canva_ptr, albedo_ptr, normal_ptr, radiance_ptr)
+    check(lib().rt_render_async(dscene.handle, C.byref(params), C.byref(tiling), C.byref(fr), stream))
+
+
+def count_async(dscene, params, tiling, counters_ptr, stream=None):
+    check(lib().rt_count_async(dscene.handle, C.byref(params), C.byref(tiling), counters_ptr, stream))
+
+
+def assemble_async(gathered_ptr, world, tile_rows, rows_per_rank, W, H, out_ptr, stream=None):
+    check(lib().rt_assemble_async(gathered_ptr, world, tile_rows, rows_per_rank, W, H, out_ptr, stream))
+
+
+def selftest_math(op, inputs, n):
+    inp = np.ascontiguousarray(inputs, dtype=np.float64)
+    out = np.zeros(n * (4 if op == 7 else 1))
+    check(lib().rt_selftest_math(op, inp.ctypes.data, out.ctypes.data, n))
+    return out
