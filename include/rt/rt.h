@@ -134,11 +134,12 @@ int rt_render_async(const rt_device_scene* scene, const rt_params* params,
                     void* hip_stream);
 
 /* Un-permute a rank-major gather of per-rank frames into a full W*H plane.
- * gathered: world * rows_per_rank * W colors, rank r's block rendered with
- * tiling {0, tile_rows, r, world, rows_per_rank/tile_rows}.  out: W*H. */
-int rt_assemble_async(const rt_color* gathered, int world, int tile_rows,
-                      int rows_per_rank, int W, int H, rt_color* out,
-                      void* hip_stream);
+ * Rank r's block starts at gathered + r*rank_stride colors (rank_stride 0:
+ * rows_per_rank*W, i.e. packed) and was rendered with tiling
+ * {0, tile_rows, r, world, rows_per_rank/tile_rows}.  out: W*H colors. */
+int rt_assemble_async(const rt_color* gathered, long long rank_stride, int world,
+                      int tile_rows, int rows_per_rank, int W, int H,
+                      rt_color* out, void* hip_stream);
 
 /* ---- instrumentation (roofline accounting, tests) ----------------------- */
 enum {

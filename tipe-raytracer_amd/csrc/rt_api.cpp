@@ -372,18 +372,21 @@ int rt_count_async(const rt_device_scene* scene, const rt_params* params, const 
     return RT_OK;
 }
 
-int rt_assemble_async(const rt_color* gathered, int world, int tile_rows, int rows_per_rank, int W, int H,
-                      rt_color* out, void* hip_stream)
+int rt_assemble_async(const rt_color* gathered, long long rank_stride, int world, int tile_rows, int rows_per_rank,
+                      int W, int H, rt_color* out, void* hip_stream)
 {
     if (!gathered || !out) return fail(RT_EINVAL, "NULL buffer");
-    if (world < 1 || tile_rows < 1 || rows_per_rank < 0 || W < 1 || H < 1 || rows_per_rank % tile_rows)
+    if (world < 1 || tile_rows < 1 || rows_per_rank < 0 || W < 1 || H < 1 || rows_per_rank % tile_rows ||
+        rank_stride < 0)
         return fail(RT_EINVAL, "bad assemble geometry");
+    if (rank_stride == 0) rank_stride = (long long)rows_per_rank * W;
+    if (rank_stride < (long long)rows_per_rank * W) return fail(RT_EINVAL, "rank_stride overlaps rank blocks");
     const long long tiles = (H + tile_rows - 1) / tile_rows;
     if ((long long)world * (rows_per_rank / tile_rows) < tiles)
         return fail(RT_EINVAL, "gather holds %d tiles/rank x %d ranks < %lld tiles", rows_per_rank / tile_rows,
                     world, tiles);
-    const int e = launch_assemble((const double*)gathered, world, tile_rows, rows_per_rank, W, H, (double*)out,
-                                  hip_stream);
+    const int e = launch_assemble((const double*)gathered, rank_stride * 3, world, tile_rows, rows_per_rank, W, H,
+                                  (double*)out, hip_stream);
     if (e) return fail(RT_EDEVICE, "assemble launch: %s", hipGetErrorString((hipError_t)e));
     return RT_OK;
 }

@@ -66,8 +66,8 @@ struct KParams {
 // launchers (rt_kernels.hip)
 int launch_render(const KParams& kp, void* stream);
 int launch_count(const KParams& kp, void* stream);
-int launch_assemble(const double* gathered, int world, int tile_rows, int rows_per_rank,
-                    int W, int H, double* out, void* stream);
+int launch_assemble(const double* gathered, long long rank_stride, int world, int tile_rows,
+                    int rows_per_rank, int W, int H, double* out, void* stream);
 int launch_selftest(int op, const double* d_in, double* d_out, int n, void* stream);
 
 }  // namespace rt

@@ -460,8 +460,9 @@ __global__ __launch_bounds__(256) void render_kernel(const KParams kp)
 }
 
 // Un-permute a rank-major gather of cyclic row tiles into the full frame.
-__global__ __launch_bounds__(256) void assemble_kernel(const double* __restrict__ gathered, int world, int tile_rows,
-                                                       int rows_per_rank, int W, int H, double* __restrict__ out)
+__global__ __launch_bounds__(256) void assemble_kernel(const double* __restrict__ gathered, long long rank_stride,
+                                                       int world, int tile_rows, int rows_per_rank, int W, int H,
+                                                       double* __restrict__ out)
 {
     const long long n = (long long)W * H * 3;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
@@ -471,7 +472,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(const double* __restrict_
         const int g = (int)(px / W), i = (int)(px - (long long)g * W);
         const int t = g / tile_rows, y = g - t * tile_rows;
         const int r = t % world, lt = t / world;
-        const long long src = ((long long)r * rows_per_rank + (long long)lt * tile_rows + y) * W + i;
+        const long long src = (long long)r * rank_stride + ((long long)lt * tile_rows + y) * W + i;
         out[e] = gathered[src * 3 + c];
     }
 }
@@ -535,14 +536,14 @@ int launch_count(const KParams& kp, void* stream)
     return (int)hipGetLastError();
 }
 
-int launch_assemble(const double* gathered, int world, int tile_rows, int rows_per_rank, int W, int H, double* out,
-                    void* stream)
+int launch_assemble(const double* gathered, long long rank_stride, int world, int tile_rows, int rows_per_rank, int W,
+                    int H, double* out, void* stream)
 {
     const long long n = (long long)W * H * 3;
     long long blocks = (n + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, gathered, world,
-                       tile_rows, rows_per_rank, W, H, out);
+    hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, gathered,
+                       rank_stride, world, tile_rows, rows_per_rank, W, H, out);
     return (int)hipGetLastError();
 }
 

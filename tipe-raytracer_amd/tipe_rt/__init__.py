@@ -32,6 +32,13 @@ def lib():
     """librt_hip.so with prototypes.  Raises if it was not built."""
     global _lib
     if _lib is None:
+        try:
+            # Share torch's bundled HIP runtime (SONAME libamdhip64.so.7): if
+            # librt_hip.so were loaded first it would pull /opt/rocm's copy
+            # and the two runtimes would contend for the device.
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RuntimeError("librt_hip.so not built (%s): run `make -C tipe-raytracer_amd` "
                                "or __graft_entry__.build(); there is no CPU fallback" % LIB_PATH)
@@ -48,8 +55,8 @@ def lib():
         L.rt_scene_release.argtypes = [C.c_void_p]
         L.rt_render_async.argtypes = [C.c_void_p, P(Params), P(Tiling), P(Frame), C.c_void_p]
         L.rt_count_async.argtypes = [C.c_void_p, P(Params), P(Tiling), C.c_void_p, C.c_void_p]
-        L.rt_assemble_async.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
-                                        C.c_void_p]
+        L.rt_assemble_async.argtypes = [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        C.c_void_p, C.c_void_p]
         L.rt_selftest_math.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         _lib = L
     return _lib
@@ -173,8 +180,9 @@ def count_async(dscene, params, tiling, counters_ptr, stream=None):
     check(lib().rt_count_async(dscene.handle, C.byref(params), C.byref(tiling), counters_ptr, stream))
 
 
-def assemble_async(gathered_ptr, world, tile_rows, rows_per_rank, W, H, out_ptr, stream=None):
-    check(lib().rt_assemble_async(gathered_ptr, world, tile_rows, rows_per_rank, W, H, out_ptr, stream))
+def assemble_async(gathered_ptr, world, tile_rows, rows_per_rank, W, H, out_ptr, stream=None, rank_stride=0):
+    check(lib().rt_assemble_async(gathered_ptr, rank_stride, world, tile_rows, rows_per_rank, W, H, out_ptr,
+                                  stream))
 
 
 def selftest_math(op, inputs, n):
