@@ -96,6 +96,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=12)
+    ap.add_argument("--chunks", type=int, default=int(os.environ.get("RT_BENCH_CHUNKS", "8")),
+                    help="rt_params.spp_chunks (fixed slice grouping of each pixel's samples)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -112,7 +114,7 @@ def main():
     spheres = scenes.cornell_spheres()
     scene = tipe_rt.make_scene(spheres)
     cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
-    p = tipe_rt.make_params(W, H, SPP, BOUNCES, cam, focus=3.0, seed=SEED)
+    p = tipe_rt.make_params(W, H, SPP, BOUNCES, cam, focus=3.0, seed=SEED, chunks=args.chunks)
     ds = tipe_rt.DeviceScene(scene, local_rank)
 
     if world == 1:
@@ -193,7 +195,8 @@ def main():
             "config": {"workload": "C2: 10-sphere Cornell box, 1200x900, 1000 spp, 6 bounces",
                        "width": W, "height": H, "spp": SPP, "bounces": BOUNCES,
                        "tile_rows": TILE_ROWS if world > 1 else H, "parallelism": "row-tiles x%d" % world,
-                       "rng": "philox4x32-10", "arith": "fp64, reference op order (bit-exact vs oracle)"},
+                       "rng": "philox4x32-10", "spp_chunks": args.chunks,
+                       "arith": "fp64, reference op order (bit-exact vs oracle)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP64_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / FP64_VECTOR_PEAK_TFLOPS, 4),
                          "traffic": traffic, "kernel": "render_kernel<false>",
@@ -207,7 +210,7 @@ def main():
             "kernel_msamples_per_s": round(launch_samples / (kernel_ms * 1e-3) / 1e6, 3),
         }
         if world == 1 and not args.no_cpu_baseline:
-            pc = tipe_rt.make_params(W, H, SPP, BOUNCES, cam, focus=3.0, seed=SEED)
+            pc = tipe_rt.make_params(W, H, SPP, BOUNCES, cam, focus=3.0, seed=SEED, chunks=args.chunks)
             rec["cpu_baseline"] = cpu_baseline(pc, scene, threads=args.cpu_threads)
             rec["speedup_vs_cpu_baseline"] = round(value / rec["cpu_baseline"]["value"], 1)
         print(json.dumps(rec))

@@ -67,12 +67,19 @@ typedef struct rt_params {
     int compat_int_truncation;         /* 1: truncate focus/ouverture/AO to int
                                           as ThreadData does (main.c:42-43)      */
     int rng;                           /* RT_RNG_*                               */
-    int reserved0;
+    int spp_chunks;                    /* 0/1: each pixel sums its samples in
+                                          order s = 0..S-1 (fill_canva's order).
+                                          P > 1: samples are summed in P fixed
+                                          contiguous slices [c*S/P, (c+1)*S/P),
+                                          then slice sums in slice order; a
+                                          deterministic grouping (independent of
+                                          GPU count) that lets one pixel's
+                                          samples run on P wavefronts          */
     unsigned long long seed;           /* Philox key                             */
 } rt_params;
 
 /* Fills defaults: RT_RNG_PHILOX, seed 1010 (main_cuda.cu's curand seed),
- * compat_int_truncation 1, everything else zero. */
+ * compat_int_truncation 1, spp_chunks 1, everything else zero. */
 void rt_params_init(rt_params* p);
 
 /* ---- lifecycle ---------------------------------------------------------- */

@@ -542,25 +542,41 @@ static void* band_worker(void* arg)
     const int W = p->largeur_image, H = p->hauteur_image, S = p->nbRayonParPixel;
     ctx c;
     init_ctx(&c, b);
+    /* rt.h spp_chunks: P > 1 sums samples in P fixed slices, then the slice
+     * sums in slice order; P = 1 is fill_canva's running sum (main.c:264-273) */
+    const int P = p->spp_chunks > 1 ? (p->spp_chunks < S ? p->spp_chunks : S) : 1;
     for (int j = b->start_row; j >= b->end_row; --j) {
         for (int i = 0; i < W; i++) {
             int pixel_index = j * W + i;
             rt_color tot[3] = {v3(0, 0, 0), v3(0, 0, 0), v3(0, 0, 0)};
-            for (int x = 0; x < S; ++x) {
-                c.pixel = (uint32_t)pixel_index;
-                c.sample = (uint32_t)x;
-                c.n = 0;
-                c.cnt[RT_CNT_SAMPLES]++;
-                double u = ((double)i + random_double(&c, -0.5, 0.5)) / (W - 1);
-                double v = ((double)j + random_double(&c, -0.5, 0.5)) / (H - 1);
-                double dx = random_double(&c, -0.5, 0.5) * b->ox;
-                double dy = random_double(&c, -0.5, 0.5) * b->oy;
-                rt_ray r = get_ray(u, v, &p->cam, b->focus, dx, dy);
-                rt_color s[3];
-                tracer(&c, r, s);
-                tot[0] = add(tot[0], s[0]);
-                tot[1] = add(tot[1], s[1]);
-                tot[2] = add(tot[2], s[2]);
+            for (int ch = 0; ch < P; ++ch) {
+                const int s0 = (int)(((long long)ch * S) / P), s1 = (int)(((long long)(ch + 1) * S) / P);
+                rt_color part[3] = {v3(0, 0, 0), v3(0, 0, 0), v3(0, 0, 0)};
+                for (int x = s0; x < s1; ++x) {
+                    c.pixel = (uint32_t)pixel_index;
+                    c.sample = (uint32_t)x;
+                    c.n = 0;
+                    c.cnt[RT_CNT_SAMPLES]++;
+                    double u = ((double)i + random_double(&c, -0.5, 0.5)) / (W - 1);
+                    double v = ((double)j + random_double(&c, -0.5, 0.5)) / (H - 1);
+                    double dx = random_double(&c, -0.5, 0.5) * b->ox;
+                    double dy = random_double(&c, -0.5, 0.5) * b->oy;
+                    rt_ray r = get_ray(u, v, &p->cam, b->focus, dx, dy);
+                    rt_color smp[3];
+                    tracer(&c, r, smp);
+                    part[0] = add(part[0], smp[0]);
+                    part[1] = add(part[1], smp[1]);
+                    part[2] = add(part[2], smp[2]);
+                }
+                if (ch == 0) {
+                    tot[0] = part[0];
+                    tot[1] = part[1];
+                    tot[2] = part[2];
+                } else {
+                    tot[0] = add(tot[0], part[0]);
+                    tot[1] = add(tot[1], part[1]);
+                    tot[2] = add(tot[2], part[2]);
+                }
             }
             b->canva[pixel_index] = write_color_canva(tot[0], S);
             if (b->albedo) b->albedo[pixel_index] = div_s(tot[1], S);

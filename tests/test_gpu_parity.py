@@ -108,6 +108,18 @@ def test_cornell_spheres_bitexact():
     check_parity(helpers.cornell(), helpers.params(64, 48, 16, 5))
 
 
+def test_cornell_spp_chunks_bitexact():
+    # spp_chunks = 4: fixed slice sums, combined in slice order (rt.h)
+    check_parity(helpers.cornell(), helpers.params(40, 30, 10, 6, chunks=4))
+
+
+def test_spp_chunks_only_move_the_last_bits():
+    bundle = helpers.cornell()
+    a = helpers.oracle_render(bundle, helpers.params(24, 18, 16, 6))
+    b = gpu_render(bundle, helpers.params(24, 18, 16, 6, chunks=8))
+    assert (helpers.rmse_per_channel(b[3], a["radiance"]) <= 1e-12).all()
+
+
 def test_cornell_six_bounces_odd_size():
     check_parity(helpers.cornell(), helpers.params(37, 29, 9, 6, seed=77))
 

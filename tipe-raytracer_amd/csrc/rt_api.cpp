@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -109,7 +110,7 @@ int validate_tiling(const rt_tiling* t)
 
 struct rt_device_scene {
     int device = 0;
-    int ns = 0, nt = 0, tw = 1, th = 1;
+    int ns = 0, ns_pad = 0, nt = 0, tw = 1, th = 1;
     long long n_texels = 0;
     SphGeo* sph = nullptr;
     DevMat* sph_mat = nullptr;
@@ -159,7 +160,7 @@ int ensure_init_locked()
     return RT_OK;
 }
 
-int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling* t, KParams& kp)
+int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling* t, KParams& kp, double* uni)
 {
     std::memset(&kp, 0, sizeof kp);
     kp.sph = sc->sph;
@@ -168,6 +169,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.tri_tex = sc->tri_tex;
     kp.texels = sc->texels;
     kp.ns = sc->ns;
+    kp.ns_pad = sc->ns_pad;
     kp.nt = sc->nt;
     kp.tw = sc->tw;
     kp.th = sc->th;
@@ -177,24 +179,28 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.S = p->nbRayonParPixel;
     kp.B = p->nbRebondMax;
     for (int i = 0; i < 3; ++i) {
-        kp.cam_o[i] = p->cam.origin.e[i];
-        kp.cam_h[i] = p->cam.horizontal.e[i];
-        kp.cam_v[i] = p->cam.vertical.e[i];
-        kp.cam_c[i] = p->cam.coin_bas_gauche.e[i];
+        uni[U_CAM_O + i] = p->cam.origin.e[i];
+        uni[U_CAM_H + i] = p->cam.horizontal.e[i];
+        uni[U_CAM_V + i] = p->cam.vertical.e[i];
+        uni[U_CAM_C + i] = p->cam.coin_bas_gauche.e[i];
     }
-    kp.focus = p->focus_distance;
-    kp.ox = p->ouverture_x;
-    kp.oy = p->ouverture_y;
-    kp.AO = p->AO_intensity;
+    double focus = p->focus_distance, ox = p->ouverture_x, oy = p->ouverture_y, AO = p->AO_intensity;
     if (p->compat_int_truncation) {     // ThreadData int fields, main.c:42-43
-        kp.focus = (double)(int)kp.focus;
-        kp.ox = (double)(int)kp.ox;
-        kp.oy = (double)(int)kp.oy;
-        kp.AO = (double)(int)kp.AO;
+        focus = (double)(int)focus;
+        ox = (double)(int)ox;
+        oy = (double)(int)oy;
+        AO = (double)(int)AO;
     }
+    uni[U_FOCUS] = focus;
+    uni[U_OX] = ox;
+    uni[U_OY] = oy;
+    uni[U_AO] = AO;
+    uni[U_WM1] = (double)(p->largeur_image - 1);    // main.c:265 (largeur_image-1)
+    uni[U_HM1] = (double)(p->hauteur_image - 1);
     kp.useAO = p->useAO ? 1 : 0;
     kp.key0 = (uint32_t)p->seed;
     kp.key1 = (uint32_t)(p->seed >> 32);
+    kp.chunks = p->spp_chunks > 1 ? std::min(p->spp_chunks, p->nbRayonParPixel) : 1;
     kp.row_base = t->row_base;
     kp.tile_rows = t->tile_rows;
     kp.tile_first = t->tile_first;
@@ -202,6 +208,42 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.n_tiles = t->n_tiles;
     kp.row_end = p->hauteur_image;
     kp.local_rows = t->n_tiles * t->tile_rows;
+    return RT_OK;
+}
+
+// Stream-ordered scratch (uniform block, chunk partials) around one launch.
+// The device's default memory pool keeps freed blocks (release threshold
+// raised once), so repeated launches do not re-map memory.
+int launch_on_stream(KParams& kp, const double* uni, hipStream_t st, bool count)
+{
+    static std::once_flag pool_once[64];
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if (dev >= 0 && dev < 64) {
+        std::call_once(pool_once[dev], [dev]() {
+            hipMemPool_t pool;
+            if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+                uint64_t thr = UINT64_MAX;
+                (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+            }
+        });
+    }
+    double* d_uni = nullptr;
+    double* d_part = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&d_uni, U_COUNT * sizeof(double), st));
+    UniBlock ub;
+    for (int i = 0; i < U_COUNT; ++i) ub.v[i] = uni[i];
+    hipError_t e = (hipError_t)launch_set_uniforms(ub, d_uni, st);
+    if (e == hipSuccess && kp.chunks > 1 && !count)
+        e = hipMallocAsync((void**)&d_part, (size_t)kp.chunks * kp.local_rows * kp.W * 9 * sizeof(double), st);
+    if (e == hipSuccess) {
+        kp.uni = d_uni;
+        kp.partial = d_part;
+        e = (hipError_t)(count ? launch_count(kp, st) : launch_render(kp, st));
+    }
+    if (d_part) (void)hipFreeAsync(d_part, st);
+    (void)hipFreeAsync(d_uni, st);
+    if (e != hipSuccess) return fail(RT_EDEVICE, "render launch: %s", hipGetErrorString(e));
     return RT_OK;
 }
 
@@ -216,6 +258,7 @@ void rt_params_init(rt_params* p)
     p->rng = RT_RNG_PHILOX;
     p->seed = 1010ull;
     p->compat_int_truncation = 1;
+    p->spp_chunks = 1;
 }
 
 int rt_init(int ndev, const int* devices)
@@ -246,7 +289,7 @@ void rt_shutdown(void)
 
 const char* rt_last_error(void) { return g_err.c_str(); }
 
-const char* rt_version(void) { return "tipe-raytracer-mi355x 0.1 (abi 1, gfx950, fp64 exact)"; }
+const char* rt_version(void) { return "tipe-raytracer-mi355x 0.2 (abi 1, gfx950, fp64 exact)"; }
 
 int rt_device_count(void)
 {
@@ -267,7 +310,10 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     DeviceGuard guard(device);
     if (!guard.ok) return fail(RT_EDEVICE, "hipSetDevice(%d) failed", device);
 
-    std::vector<SphGeo> sph((size_t)scene->nbSpheres);
+    // Spheres padded to an even count with never-hit records (r2 = -inf makes
+    // the discriminant -inf): the kernel reads them two per s_load_dwordx16.
+    const int ns_pad = (scene->nbSpheres + 1) & ~1;
+    std::vector<SphGeo> sph((size_t)ns_pad, SphGeo{0.0, 0.0, 0.0, -HUGE_VAL});
     std::vector<DevMat> sph_mat((size_t)scene->nbSpheres);
     for (int i = 0; i < scene->nbSpheres; ++i) {
         const rt_sphere& s = scene->sphere_list[i];
@@ -320,6 +366,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     rt_device_scene* ds = new rt_device_scene();
     ds->device = device;
     ds->ns = scene->nbSpheres;
+    ds->ns_pad = ns_pad;
     ds->nt = scene->nbTriangles;
     ds->tw = scene->nbTriangles > 0 ? scene->tex_width : 1;
     ds->th = scene->nbTriangles > 0 ? scene->tex_height : 1;
@@ -343,16 +390,15 @@ int rt_render_async(const rt_device_scene* scene, const rt_params* params, const
     if ((rc = validate_params(params)) || (rc = validate_tiling(tiling))) return rc;
     if (!frame || !frame->canva) return fail(RT_EINVAL, "frame.canva is NULL");
     KParams kp;
-    make_kparams(scene, params, tiling, kp);
+    double uni[U_COUNT];
+    make_kparams(scene, params, tiling, kp, uni);
     kp.canva = (double*)frame->canva;
     kp.albedo = (double*)frame->albedo;
     kp.normal = (double*)frame->normal;
     kp.radiance = (double*)frame->radiance;
     if (kp.local_rows == 0 || kp.W == 0) return RT_OK;
     DeviceGuard guard(scene->device);
-    const int e = launch_render(kp, hip_stream);
-    if (e) return fail(RT_EDEVICE, "render launch: %s", hipGetErrorString((hipError_t)e));
-    return RT_OK;
+    return launch_on_stream(kp, uni, (hipStream_t)hip_stream, false);
 }
 
 int rt_count_async(const rt_device_scene* scene, const rt_params* params, const rt_tiling* tiling,
@@ -363,13 +409,12 @@ int rt_count_async(const rt_device_scene* scene, const rt_params* params, const 
     if ((rc = validate_params(params)) || (rc = validate_tiling(tiling))) return rc;
     if (!d_counters) return fail(RT_EINVAL, "d_counters is NULL");
     KParams kp;
-    make_kparams(scene, params, tiling, kp);
+    double uni[U_COUNT];
+    make_kparams(scene, params, tiling, kp, uni);
     kp.counters = d_counters;
     if (kp.local_rows == 0) return RT_OK;
     DeviceGuard guard(scene->device);
-    const int e = launch_count(kp, hip_stream);
-    if (e) return fail(RT_EDEVICE, "count launch: %s", hipGetErrorString((hipError_t)e));
-    return RT_OK;
+    return launch_on_stream(kp, uni, (hipStream_t)hip_stream, true);
 }
 
 int rt_assemble_async(const rt_color* gathered, long long rank_stride, int world, int tile_rows, int rows_per_rank,
@@ -385,7 +430,7 @@ int rt_assemble_async(const rt_color* gathered, long long rank_stride, int world
     if ((long long)world * (rows_per_rank / tile_rows) < tiles)
         return fail(RT_EINVAL, "gather holds %d tiles/rank x %d ranks < %lld tiles", rows_per_rank / tile_rows,
                     world, tiles);
-    const int e = launch_assemble((const double*)gathered, rank_stride * 3, world, tile_rows, rows_per_rank, W, H,
+    const int e = launch_assemble((const double*)gathered, rank_stride, world, tile_rows, rows_per_rank, W, H,
                                   (double*)out, hip_stream);
     if (e) return fail(RT_EDEVICE, "assemble launch: %s", hipGetErrorString((hipError_t)e));
     return RT_OK;
@@ -449,15 +494,15 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, i
         }
         rt_tiling t{row_lo, k, q, ndev, s.n_tiles};
         KParams kp;
-        make_kparams(s.sc, params, &t, kp);
+        double uni[U_COUNT];
+        make_kparams(s.sc, params, &t, kp, uni);
         kp.row_end = row_hi + 1;
         kp.canva = s.buf;
         kp.albedo = albedo ? s.buf + s.plane : nullptr;
         kp.normal = normal ? s.buf + 2 * s.plane : nullptr;
-        const int le = launch_render(kp, s.st);
-        if (le) {
+        if ((rc = launch_on_stream(kp, uni, s.st, false))) {
             cleanup();
-            return fail(RT_EDEVICE, "render launch: %s", hipGetErrorString((hipError_t)le));
+            return rc;
         }
     }
     std::vector<double> host;

@@ -3,20 +3,75 @@
 // "Portable math").  Built only from IEEE-754 +,-,*,/,sqrt, rint and bit
 // casts, compiled with -ffp-contract=off, so results are bit-identical to the
 // CPU restatement in oracle/pm_math.h.
+//
+// Register pressure: the ~60 FP64 coefficients live in a __constant__ table
+// read through the scalar unit (s_load) at the point of use; the table index
+// is laundered through an empty asm so LICM cannot hoist the loads out of the
+// bounce/sample loops and pin 120 SGPRs (that pressure spilled into VGPR
+// lanes and capped occupancy at 2 waves/SIMD in the first kernel).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
 namespace rt {
 
+typedef const double __attribute__((address_space(4)))* cdptr;
+
+// Opaque wave-uniform zero: defeats loop-invariant hoisting of what uses it.
+__device__ __forceinline__ int opq0()
+{
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    return z;
+}
+
+enum : int {
+    // sin/cos (Taylor to degree 17 / 16 on |r| <= pi/4)
+    KC_TWO_OVER_PI = 0, KC_PIO2_1, KC_PIO2_2, KC_PIO2_3,
+    KC_S1, KC_S2, KC_S3, KC_S4, KC_S5, KC_S6, KC_S7, KC_S8,
+    KC_C1, KC_C2, KC_C3, KC_C4, KC_C5, KC_C6, KC_C7, KC_C8,
+    // acos (fdlibm)
+    KC_PIO2_HI, KC_PIO2_LO, KC_PI,
+    KC_PS0, KC_PS1, KC_PS2, KC_PS3, KC_PS4, KC_PS5, KC_QS1, KC_QS2, KC_QS3, KC_QS4,
+    // log / exp
+    KC_SQRT2, KC_L1, KC_L2, KC_L3, KC_L4, KC_L5, KC_L6, KC_L7, KC_L8, KC_L9, KC_L10, KC_L11,
+    KC_LN2_HI, KC_LN2_LO, KC_INV_LN2, KC_LN2,
+    KC_E2, KC_E3, KC_E4, KC_E5, KC_E6, KC_E7, KC_E8, KC_E9, KC_E10, KC_E11, KC_E12, KC_E13,
+    KC_COUNT
+};
+
+__constant__ const double kC[KC_COUNT] = {
+    0x1.45f306dc9c883p-1, 0x1.921fb54400000p+0, 0x1.0b4611a600000p-34, 0x1.3198a2e000000p-69,
+    -0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19,
+    -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49,
+    -0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16,
+    -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45,
+    0x1.921fb54442d18p+0, 0x1.1a62633145c07p-54, 0x1.921fb54442d18p+1,
+    0x1.5555555555555p-3, -0x1.4d61203eb6f7dp-2, 0x1.9c1550e884455p-3, -0x1.48228b5688f3bp-5,
+    0x1.9efe07501b288p-11, 0x1.23de10dfdf709p-15, -0x1.33a271c8a2d4bp+1, 0x1.02ae59c598ac8p+1,
+    -0x1.6066c1b8d0159p-1, 0x1.3b8c5b12e9282p-4,
+    0x1.6a09e667f3bcdp+0, 0x1.5555555555555p-2, 0x1.999999999999ap-3, 0x1.2492492492492p-3,
+    0x1.c71c71c71c71cp-4, 0x1.745d1745d1746p-4, 0x1.3b13b13b13b14p-4, 0x1.1111111111111p-4,
+    0x1.e1e1e1e1e1e1ep-5, 0x1.af286bca1af28p-5, 0x1.8618618618618p-5, 0x1.642c8590b2164p-5,
+    0x1.62e42fee00000p-1, 0x1.a39ef35793c76p-33, 0x1.71547652b82fep+0, 0x1.62e42fefa39efp-1,
+    0x1.0000000000000p-1, 0x1.5555555555555p-3, 0x1.5555555555555p-5, 0x1.1111111111111p-7,
+    0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-13, 0x1.a01a01a01a01ap-16, 0x1.71de3a556c734p-19,
+    0x1.27e4fb7789f5cp-22, 0x1.ae64567f544e4p-26, 0x1.1eed8eff8d898p-29, 0x1.6124613a86d09p-33,
+};
+
+// Scalar load of constant i (index laundered through b = opq0()).
+#define KCV(b, i) (((cdptr)kC)[(b) + (i)])
+
 // ---- Philox4x32-10 (Random123 / rocrand_philox4x32_10 engine) -------------
 struct Philox {
     uint32_t w0, w1, w2, w3;
 };
 
+template <bool UNIFORM_KEY = true>
 __device__ __forceinline__ Philox philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                 uint32_t k0, uint32_t k1)
 {
+    if (UNIFORM_KEY) asm volatile("" : "+s"(k0), "+s"(k1));   // key schedule in place (SALU), not hoisted
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
@@ -54,16 +109,15 @@ __device__ __forceinline__ double unit31(uint32_t r) { return (double)r / 214748
 // ---- sin / cos of a float, evaluated in double, rounded to float ----------
 __device__ __forceinline__ int pm_sincos(float x, double& s, double& c)
 {
+    const int b = opq0();
     const double xd = (double)x;
-    const double kd = rint(xd * 0x1.45f306dc9c883p-1);
-    const double r = ((xd - kd * 0x1.921fb54400000p+0) - kd * 0x1.0b4611a600000p-34) - kd * 0x1.3198a2e000000p-69;
+    const double kd = rint(xd * KCV(b, KC_TWO_OVER_PI));
+    const double r = ((xd - kd * KCV(b, KC_PIO2_1)) - kd * KCV(b, KC_PIO2_2)) - kd * KCV(b, KC_PIO2_3);
     const double z = r * r;
-    const double ps = -0x1.5555555555555p-3 + z * (0x1.1111111111111p-7 + z * (-0x1.a01a01a01a01ap-13 +
-                      z * (0x1.71de3a556c734p-19 + z * (-0x1.ae64567f544e4p-26 + z * (0x1.6124613a86d09p-33 +
-                      z * (-0x1.ae7f3e733b81fp-41 + z * 0x1.952c77030ad4ap-49))))));
-    const double pc = -0x1.0000000000000p-1 + z * (0x1.5555555555555p-5 + z * (-0x1.6c16c16c16c17p-10 +
-                      z * (0x1.a01a01a01a01ap-16 + z * (-0x1.27e4fb7789f5cp-22 + z * (0x1.1eed8eff8d898p-29 +
-                      z * (-0x1.93974a8c07c9dp-37 + z * 0x1.ae7f3e733b81fp-45))))));
+    const double ps = KCV(b, KC_S1) + z * (KCV(b, KC_S2) + z * (KCV(b, KC_S3) + z * (KCV(b, KC_S4) +
+                      z * (KCV(b, KC_S5) + z * (KCV(b, KC_S6) + z * (KCV(b, KC_S7) + z * KCV(b, KC_S8)))))));
+    const double pc = KCV(b, KC_C1) + z * (KCV(b, KC_C2) + z * (KCV(b, KC_C3) + z * (KCV(b, KC_C4) +
+                      z * (KCV(b, KC_C5) + z * (KCV(b, KC_C6) + z * (KCV(b, KC_C7) + z * KCV(b, KC_C8)))))));
     s = r + (r * z) * ps;
     c = 1.0 + z * pc;
     return (int)((long long)kd & 3);
@@ -80,18 +134,18 @@ __device__ __forceinline__ void pm_sincosf(float x, float& sn, float& cs)
 }
 
 // ---- acos (fdlibm scheme) --------------------------------------------------
-__device__ __forceinline__ double pm_acos_R(double z)
+__device__ __forceinline__ double pm_acos_R(int b, double z)
 {
-    const double p = z * (0x1.5555555555555p-3 + z * (-0x1.4d61203eb6f7dp-2 + z * (0x1.9c1550e884455p-3 +
-                     z * (-0x1.48228b5688f3bp-5 + z * (0x1.9efe07501b288p-11 + z * 0x1.23de10dfdf709p-15)))));
-    const double q = 1.0 + z * (-0x1.33a271c8a2d4bp+1 + z * (0x1.02ae59c598ac8p+1 +
-                     z * (-0x1.6066c1b8d0159p-1 + z * 0x1.3b8c5b12e9282p-4)));
+    const double p = z * (KCV(b, KC_PS0) + z * (KCV(b, KC_PS1) + z * (KCV(b, KC_PS2) +
+                     z * (KCV(b, KC_PS3) + z * (KCV(b, KC_PS4) + z * KCV(b, KC_PS5))))));
+    const double q = 1.0 + z * (KCV(b, KC_QS1) + z * (KCV(b, KC_QS2) + z * (KCV(b, KC_QS3) + z * KCV(b, KC_QS4))));
     return p / q;
 }
 
 __device__ __forceinline__ double pm_acos(double x)
 {
-    constexpr double PIO2_HI = 0x1.921fb54442d18p+0, PIO2_LO = 0x1.1a62633145c07p-54, PI = 0x1.921fb54442d18p+1;
+    const int b = opq0();
+    const double PIO2_HI = KCV(b, KC_PIO2_HI), PIO2_LO = KCV(b, KC_PIO2_LO), PI = KCV(b, KC_PI);
     const unsigned long long u = (unsigned long long)__double_as_longlong(x);
     const uint32_t hx = (uint32_t)(u >> 32);
     const uint32_t ix = hx & 0x7fffffffu;
@@ -101,12 +155,12 @@ __device__ __forceinline__ double pm_acos(double x)
     }
     if (ix < 0x3fe00000u) {
         if (ix <= 0x3c600000u) return PIO2_HI + PIO2_LO;
-        const double r = pm_acos_R(x * x);
+        const double r = pm_acos_R(b, x * x);
         return PIO2_HI - (x - (PIO2_LO - x * r));
     }
     if (hx >> 31) {
         const double z = (1.0 + x) * 0.5;
-        const double r = pm_acos_R(z);
+        const double r = pm_acos_R(b, z);
         const double s = sqrt(z);
         const double w = r * s - PIO2_LO;
         return PI - 2.0 * (s + w);
@@ -115,7 +169,7 @@ __device__ __forceinline__ double pm_acos(double x)
     const double s = sqrt(z);
     const double df = __longlong_as_double((long long)((unsigned long long)__double_as_longlong(s) & 0xffffffff00000000ull));
     const double c = (z - df * df) / (s + df);
-    const double r = pm_acos_R(z);
+    const double r = pm_acos_R(b, z);
     const double w = r * s + c;
     return 2.0 * (df + w);
 }
@@ -123,35 +177,33 @@ __device__ __forceinline__ double pm_acos(double x)
 // ---- pow ---------------------------------------------------------------------
 __device__ __forceinline__ double pm_from_bits(unsigned long long b) { return __longlong_as_double((long long)b); }
 
-__device__ __forceinline__ double pm_log(double x)
+__device__ __forceinline__ double pm_log(int b, double x)
 {
     const unsigned long long u = (unsigned long long)__double_as_longlong(x);
     int e = (int)((u >> 52) & 0x7ff) - 1023;
     double m = pm_from_bits((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
-    if (m > 0x1.6a09e667f3bcdp+0) { m = m * 0.5; e = e + 1; }
+    if (m > KCV(b, KC_SQRT2)) { m = m * 0.5; e = e + 1; }
     const double f = m - 1.0;
     const double s = f / (2.0 + f);
     const double z = s * s;
-    const double t = 0x1.5555555555555p-2 + z * (0x1.999999999999ap-3 + z * (0x1.2492492492492p-3 +
-                     z * (0x1.c71c71c71c71cp-4 + z * (0x1.745d1745d1746p-4 + z * (0x1.3b13b13b13b14p-4 +
-                     z * (0x1.1111111111111p-4 + z * (0x1.e1e1e1e1e1e1ep-5 + z * (0x1.af286bca1af28p-5 +
-                     z * (0x1.8618618618618p-5 + z * 0x1.642c8590b2164p-5)))))))));
+    const double t = KCV(b, KC_L1) + z * (KCV(b, KC_L2) + z * (KCV(b, KC_L3) + z * (KCV(b, KC_L4) +
+                     z * (KCV(b, KC_L5) + z * (KCV(b, KC_L6) + z * (KCV(b, KC_L7) + z * (KCV(b, KC_L8) +
+                     z * (KCV(b, KC_L9) + z * (KCV(b, KC_L10) + z * KCV(b, KC_L11))))))))));
     const double lm = 2.0 * s + (2.0 * s) * (z * t);
     const double ed = (double)e;
-    return ed * 0x1.62e42fee00000p-1 + (lm + ed * 0x1.a39ef35793c76p-33);
+    return ed * KCV(b, KC_LN2_HI) + (lm + ed * KCV(b, KC_LN2_LO));
 }
 
-__device__ __forceinline__ double pm_exp(double t)
+__device__ __forceinline__ double pm_exp(int b, double t)
 {
     if (t > 709.0) return __longlong_as_double(0x7ff0000000000000ll);
     if (t < -708.0) return 0.0;
-    const double kd = rint(t * 0x1.71547652b82fep+0);
-    const double r = (t - kd * 0x1.62e42fee00000p-1) - kd * 0x1.a39ef35793c76p-33;
-    const double p = 1.0 + r * (1.0 + r * (0x1.0000000000000p-1 + r * (0x1.5555555555555p-3 +
-                     r * (0x1.5555555555555p-5 + r * (0x1.1111111111111p-7 + r * (0x1.6c16c16c16c17p-10 +
-                     r * (0x1.a01a01a01a01ap-13 + r * (0x1.a01a01a01a01ap-16 + r * (0x1.71de3a556c734p-19 +
-                     r * (0x1.27e4fb7789f5cp-22 + r * (0x1.ae64567f544e4p-26 + r * (0x1.1eed8eff8d898p-29 +
-                     r * 0x1.6124613a86d09p-33))))))))))));
+    const double kd = rint(t * KCV(b, KC_INV_LN2));
+    const double r = (t - kd * KCV(b, KC_LN2_HI)) - kd * KCV(b, KC_LN2_LO);
+    const double p = 1.0 + r * (1.0 + r * (KCV(b, KC_E2) + r * (KCV(b, KC_E3) + r * (KCV(b, KC_E4) +
+                     r * (KCV(b, KC_E5) + r * (KCV(b, KC_E6) + r * (KCV(b, KC_E7) + r * (KCV(b, KC_E8) +
+                     r * (KCV(b, KC_E9) + r * (KCV(b, KC_E10) + r * (KCV(b, KC_E11) + r * (KCV(b, KC_E12) +
+                     r * KCV(b, KC_E13)))))))))))));
     const int k = (int)kd;
     const int k1 = k / 2, k2 = k - k1;
     const double s1 = pm_from_bits((unsigned long long)(k1 + 1023) << 52);
@@ -173,13 +225,14 @@ __device__ __forceinline__ double pm_pow(double x, double y)
         }
         return n < 0 ? 1.0 / res : res;
     }
+    const int b = opq0();
     const double inf = __longlong_as_double(0x7ff0000000000000ll);
     if (x != x || y != y) return x + y;
     if (x == 0.0) return y > 0.0 ? 0.0 : inf;
     if (x < 0.0) return (x - x) / (x - x);
     if (x == inf) return y > 0.0 ? inf : 0.0;
-    if (x < 0x1p-1022) return pm_exp(y * (pm_log(x * 0x1p54) - 54.0 * 0x1.62e42fefa39efp-1));
-    return pm_exp(y * pm_log(x));
+    if (x < 0x1p-1022) return pm_exp(b, y * (pm_log(b, x * 0x1p54) - 54.0 * KCV(b, KC_LN2)));
+    return pm_exp(b, y * pm_log(b, x));
 }
 
 }  // namespace rt

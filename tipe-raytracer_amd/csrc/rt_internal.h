@@ -2,11 +2,17 @@
 // the C-ABI (rt_api.cpp) and the kernels (rt_kernels.hip).
 //
 // HBM layout of one uploaded scene (DESIGN.md "Data layout"):
-//   SphGeo  [ns]  32 B   center, radius^2      — read wave-uniformly (SMEM)
-//   DevMat  [ns]  80 B   sphere material       — gathered for the winner only
-//   TriGeo  [nt]  96 B   A, B-A, C-A, N        — read wave-uniformly (SMEM)
-//   TriTex  [nt]  112 B  B, C, uvA/B/C, mat    — gathered for the winner only
-//   DevMat  [nm*th*tw]   texel table (reference `material` records)
+//   SphGeo  [ns_pad] 32 B  center, radius^2 — scanned wave-uniformly through
+//                          the scalar unit, two records per s_load_dwordx16;
+//                          padded to an even count with never-hit records
+//                          (radius^2 = -inf => discriminant = -inf)
+//   DevMat  [ns]     80 B  sphere material — gathered for the winner only
+//   TriGeo  [nt]     96 B  A, B-A, C-A, N  — scanned wave-uniformly
+//   TriTex  [nt]    104 B  B, C, uvA/B/C, material — winner only
+//   DevMat  [nm*th*tw]     texel table (reference `material` records)
+// Per launch: a 18-double uniform block (camera, focus, aperture, AO, W-1,
+// H-1) read through the scalar unit where used, and, when the samples of a
+// pixel are split over P chunks, a [P][pixels][9] partial-sum scratch.
 #pragma once
 #include <cstdint>
 
@@ -35,6 +41,13 @@ static_assert(sizeof(DevMat) == 80, "DevMat");
 static_assert(sizeof(TriGeo) == 96, "TriGeo");
 static_assert(sizeof(TriTex) == 104, "TriTex");
 
+// uniform block (doubles)
+enum : int {
+    U_CAM_O = 0, U_CAM_H = 3, U_CAM_V = 6, U_CAM_C = 9,
+    U_FOCUS = 12, U_OX, U_OY, U_AO, U_WM1, U_HM1,
+    U_COUNT
+};
+
 // Everything one render launch needs, passed by value as the kernel argument.
 struct KParams {
     // scene
@@ -43,15 +56,15 @@ struct KParams {
     const TriGeo* tri;
     const TriTex* tri_tex;
     const DevMat* texels;
-    int ns, nt;
+    const double* uni;       // U_COUNT doubles
+    int ns, ns_pad, nt;
     int tw, th;
     long long n_texels;
     // image / integrator
     int W, H, S, B;
-    double cam_o[3], cam_h[3], cam_v[3], cam_c[3];
-    double focus, ox, oy, AO;
     int useAO;
     uint32_t key0, key1;
+    int chunks;              // samples of a pixel split into this many chunks
     // tiling
     int row_base, tile_rows, tile_first, tile_step, n_tiles, row_end;
     int local_rows;          // n_tiles * tile_rows
@@ -60,10 +73,14 @@ struct KParams {
     double* albedo;
     double* normal;
     double* radiance;
+    double* partial;         // chunks > 1: [chunks][local_rows*W][9]
     unsigned long long* counters;
 };
 
+struct UniBlock { double v[U_COUNT]; };
+
 // launchers (rt_kernels.hip)
+int launch_set_uniforms(const UniBlock& u, double* d_uni, void* stream);
 int launch_render(const KParams& kp, void* stream);
 int launch_count(const KParams& kp, void* stream);
 int launch_assemble(const double* gathered, long long rank_stride, int world, int tile_rows,

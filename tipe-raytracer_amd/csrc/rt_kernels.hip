@@ -1,31 +1,43 @@
 // rt_kernels.hip — the per-pixel path-tracing kernel for gfx950 (CDNA4).
 //
-// One thread renders one pixel: the nbRayonParPixel sample loop, the
-// nbRebondMax bounce loop, closest-hit scans, shading and AO all run in
-// registers; the only HBM traffic is the final 3-4 colors per pixel.
+// One thread renders one pixel (or one chunk of its samples): the sample
+// loop, the nbRebondMax bounce loop, closest-hit scans, shading and AO all
+// run in registers; HBM traffic is the final colors per pixel (plus, with
+// sample chunking, one 72-byte partial sum per pixel and chunk).
 //
 // Semantics follow main.c (the authoritative CPU path), not main_cuda.cu:
-//   fill_canva        main.c:245-284      -> render_kernel
+//   fill_canva        main.c:245-284      -> render_kernel / combine_kernel
 //   tracer            main.c:118-242      -> trace()
 //   closest_hit       main.c:52-92        -> closest_hit()
 //   ambient_occlusion main.c:94-116       -> ao_factor()
-//   hit_sphere        sphere.h:13-47, hit_triangle mesh.h:70-94,
-//   tri_uvmapping     texture.h:44-90, get_ray camera.h:42-55,
-//   random_dir_no_norm / refracted_vec / hsl  rtutility.h:81-231,
-//   write_color_canva rtutility.h:56-71
-// Every floating-point operation is the reference's, in its association
-// order, one IEEE rounding each (built with -ffp-contract=off): results are
-// bit-identical to the CPU restatement in RT_RNG_PHILOX mode.
+//   hit_sphere        sphere.h:13-47      -> sphere_exact() (+ candidate pass)
+//   hit_triangle      mesh.h:70-94, tri_uvmapping texture.h:44-90,
+//   get_ray           camera.h:42-55, random_dir_no_norm / refracted_vec /
+//   hsl               rtutility.h:81-231, write_color_canva rtutility.h:56-71
+// Every floating-point value that reaches an output is produced by the
+// reference's IEEE operations in its association order, one rounding each
+// (-ffp-contract=off): results are bit-identical to the CPU restatement in
+// RT_RNG_PHILOX mode.
 //
 // MI355X mapping (DESIGN.md "Kernel"):
-//  * geometry is scanned in the same order by every lane of a wave, so the
-//    sphere/triangle records are read through constant-address-space
-//    pointers -> scalar (SMEM) loads into SGPRs, broadcast to 64 lanes for
-//    free; nothing is staged per lane;
+//  * geometry is scanned in the same order by every lane of a wave: sphere
+//    records come through the scalar unit (SMEM -> SGPRs, broadcast to the
+//    64 lanes for free), two per s_load_dwordx16;
+//  * closest hit = a cheap candidate pass (hardware rsq + one Newton step,
+//    reciprocal multiply, rigorous error intervals) followed by the exact
+//    reference arithmetic for the single winner; any interval overlap or
+//    threshold ambiguity falls back to the exact scan for that ray, so the
+//    result never depends on the approximation;
 //  * per-lane divergent data (the winner's material, texels) is fetched once
 //    per bounce from L1/L2;
 //  * the IOR stack of pile.h reduces to one register (top n2), see trace();
-//  * 256-thread blocks = four 8x8-pixel waves (ray coherence), 16x16 tiles.
+//  * albedo/normal are final once the primary chain (camera ray through
+//    alpha holes) ends, so they are added to the accumulators there instead
+//    of being carried through the bounce loop;
+//  * 256-thread blocks = four 8x8-pixel waves (ray coherence); grid.z splits
+//    each pixel's samples into `chunks` fixed slices for load balance, summed
+//    in chunk order by combine_kernel (a deterministic, GPU-count-independent
+//    grouping that the oracle reproduces).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -33,9 +45,11 @@
 #include "rt_internal.h"
 #include "rt_device_math.h"
 
-namespace rt {
+#ifndef RT_WAVES_PER_SIMD
+#define RT_WAVES_PER_SIMD 4
+#endif
 
-#define RT_CONST __attribute__((address_space(4)))
+namespace rt {
 
 struct V3 {
     double x, y, z;
@@ -63,6 +77,17 @@ __device__ __forceinline__ Mat load_mat(const DevMat* m)
     return Mat{v3(r.dr, r.dg, r.db), v3(r.er, r.eg, r.eb), r.es, r.rs, r.alpha, r.ior};
 }
 
+// Per-pixel sums (radiance, albedo, normal) live in LDS, one 9-double column
+// per thread ([9][256], conflict-free), so they occupy no VGPRs across the
+// bounce loop.  Only the owning thread touches its column: plain
+// read-add-write, same IEEE adds in the same order as fill_canva's sums.
+__device__ __forceinline__ void acc_add(double* acc, int base, V3 v)
+{
+    acc[(base + 0) * 256] = acc[(base + 0) * 256] + v.x;
+    acc[(base + 1) * 256] = acc[(base + 1) * 256] + v.y;
+    acc[(base + 2) * 256] = acc[(base + 2) * 256] + v.z;
+}
+
 // Per-thread event counters (COUNT instantiation only).
 struct Cnt {
     unsigned long long c[RT_NCOUNTERS];
@@ -70,56 +95,146 @@ struct Cnt {
 
 enum : int { HIT_NONE = 0, HIT_SPHERE = 1, HIT_TRI = 2 };
 
-// closest_hit, main.c:52-92: linear scan, spheres then triangles; a strictly
-// closer hit replaces the record.  Returns the winner (kind, index, t).
+__device__ __forceinline__ double dinf() { return __longlong_as_double(0x7ff0000000000000ll); }
+
+// hit_sphere, sphere.h:13-47, exact reference arithmetic.  two_a = 2*a and
+// four_a = 4*a with a = dot(d, d) (`4*a*c` == (4*a)*c).  A negative
+// numerator decides t < 1e-4 without the division (2a > 0).
+__device__ __forceinline__ bool sphere_exact(double cx, double cy, double cz, double r2, const V3 o, const V3 d,
+                                             double two_a, double four_a, double& t)
+{
+    const double ocx = o.x - cx, ocy = o.y - cy, ocz = o.z - cz;
+    const double b = 2.0 * (ocx * d.x + ocy * d.y + ocz * d.z);
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
+    const double disc = b * b - four_a * c;
+    if (!(disc > 0)) return false;
+    const double sq = sqrt(disc);
+    const double n1 = -b - sq;
+    if (!(n1 < 0.0)) {
+        t = n1 / two_a;
+        if (t >= 0.0001) return true;
+    }
+    const double n2 = -b + sq;
+    if (!(n2 < 0.0)) {
+        t = n2 / two_a;
+        if (t >= 0.0001) return true;
+    }
+    return false;
+}
+
+// Closest sphere (main.c:59-78).  Candidate pass with error intervals, then
+// the exact test for the winner; exact scan on any ambiguity.
+//
+// Interval bound (DESIGN.md "Exact closest hit"): sa = disc*r1 with r1 one
+// Newton step from v_rsq_f64 has |sa/sqrt(disc) - 1| <= 2^-45 (measured
+// 2^-47.7 over 1e9 inputs; v_rsq_f64 <= 2^-24.2), so with q = RN(n_a*inv2a)
+// the exact root t satisfies |t - q| <= sa*inv2a*2^-39.7 + |q|*2^-50; the
+// margin used, sa*inv2a*2^-39 + |q|*2^-49, also absorbs the rounding of the
+// interval end points.
+template <bool COUNT>
+__device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, const V3 d, double two_a,
+                                               double four_a, double inv2a, double& t_best, Cnt& cnt)
+{
+    const cdptr sg = (cdptr)kp.sph;
+    const double INF = dinf();
+    double blo = INF, bhi = INF;
+    int bk = -1;
+    bool amb = false;
+    for (int k = 0; k < kp.ns_pad; k += 2) {
+        double g[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = sg[4 * k + j];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const double ocx = o.x - g[4 * h], ocy = o.y - g[4 * h + 1], ocz = o.z - g[4 * h + 2];
+            const double b = 2.0 * (ocx * d.x + ocy * d.y + ocz * d.z);
+            const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - g[4 * h + 3];
+            const double disc = b * b - four_a * c;
+            if (disc > 0) {
+                if (COUNT) cnt.c[RT_CNT_SPHERE_DISC] += 1;
+                if (!(disc >= 0x1p-900 && disc <= 0x1p900)) {
+                    amb = true;
+                    continue;
+                }
+                const double r0 = __builtin_amdgcn_rsq(disc);
+                const double r1 = r0 * (1.5 - (0.5 * disc) * (r0 * r0));
+                const double sa = disc * r1;
+                const double sm = (sa * inv2a) * 0x1p-39;
+                double lo = 0.0, hi = 0.0;
+                bool cand = false;
+                const double q1 = (-b - sa) * inv2a;
+                const double m1 = sm + fabs(q1) * 0x1p-49;
+                if (q1 - m1 >= 0.0001) {
+                    lo = q1 - m1;
+                    hi = q1 + m1;
+                    cand = true;
+                } else if (q1 + m1 < 0.0001) {
+                    const double q2 = (-b + sa) * inv2a;
+                    const double m2 = sm + fabs(q2) * 0x1p-49;
+                    if (q2 - m2 >= 0.0001) {
+                        lo = q2 - m2;
+                        hi = q2 + m2;
+                        cand = true;
+                    } else if (!(q2 + m2 < 0.0001)) {
+                        amb = true;
+                    }
+                } else {
+                    amb = true;
+                }
+                if (cand) {
+                    if (hi < blo) {
+                        blo = lo;
+                        bhi = hi;
+                        bk = k + h;
+                    } else if (!(lo >= bhi)) {
+                        amb = true;
+                    }
+                }
+            }
+        }
+    }
+    double t = INF;
+    int win = -1;
+    if (!amb && bk >= 0) {
+        const SphGeo s = kp.sph[bk];
+        if (sphere_exact(s.cx, s.cy, s.cz, s.r2, o, d, two_a, four_a, t)) win = bk;
+        else amb = true;     // cannot happen within the bound; stay exact anyway
+    }
+    if (amb) {               // exact reference scan for this ray
+        t = INF;
+        win = -1;
+        for (int k = 0; k < kp.ns_pad; ++k) {
+            double tk;
+            if (sphere_exact(sg[4 * k], sg[4 * k + 1], sg[4 * k + 2], sg[4 * k + 3], o, d, two_a, four_a, tk) &&
+                tk < t) {
+                t = tk;
+                win = k;
+            }
+        }
+    }
+    t_best = t;
+    return win;
+}
+
+// closest_hit, main.c:52-92: spheres, then triangles; a strictly closer hit
+// replaces the record.  Returns the winner (kind, index, t).
 template <bool COUNT>
 __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const V3 d, double& t_best, int& idx,
                                            Cnt& cnt)
 {
-    const SphGeo* __restrict__ sph = kp.sph;
-    const TriGeo* __restrict__ tri = kp.tri;
     const double a = dot(d, d);          // sphere.h:20 (same for every sphere)
     const double two_a = 2 * a;          // sphere.h:27,36
-    const double four_a = 4 * a;         // sphere.h:24 `4*a*c` == (4*a)*c
-    double best = __longlong_as_double(0x7ff0000000000000ll);   // INFINITY, main.c:56
-    int kind = HIT_NONE, win = -1;
+    const double four_a = 4 * a;         // sphere.h:24
+    const double inv2a = 1.0 / two_a;    // candidate pass only
     if (COUNT) {
         cnt.c[RT_CNT_CASTS] += 1;
         cnt.c[RT_CNT_SPHERE_TESTS] += (unsigned long long)kp.ns;
         cnt.c[RT_CNT_TRI_TESTS] += (unsigned long long)kp.nt;
     }
-    for (int k = 0; k < kp.ns; ++k) {                     // hit_sphere, sphere.h:13-47
-        const SphGeo s = sph[k];
-        const double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
-        const double b = 2.0 * (ocx * d.x + ocy * d.y + ocz * d.z);
-        const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
-        const double disc = b * b - four_a * c;
-        if (disc > 0) {
-            if (COUNT) cnt.c[RT_CNT_SPHERE_DISC] += 1;
-            const double sq = sqrt(disc);
-            // t1 = (-b - sq)/(2a) is taken iff t1 >= 1e-4; a negative
-            // numerator decides that without the division (2a > 0).
-            const double n1 = -b - sq;
-            double t = 0.0;
-            bool hit = false;
-            if (!(n1 < 0.0)) {
-                t = n1 / two_a;
-                hit = t >= 0.0001;
-            }
-            if (!hit) {
-                const double n2 = -b + sq;
-                if (!(n2 < 0.0)) {
-                    t = n2 / two_a;
-                    hit = t >= 0.0001;
-                }
-            }
-            if (hit && t < best) {
-                best = t;
-                kind = HIT_SPHERE;
-                win = k;
-            }
-        }
-    }
+    double best;
+    int win = spheres_closest<COUNT>(kp, o, d, two_a, four_a, inv2a, best, cnt);
+    int kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
+    const TriGeo* __restrict__ tri = kp.tri;
     for (int k = 0; k < kp.nt; ++k) {                     // hit_triangle, mesh.h:70-94
         const TriGeo g = tri[k];
         const double det = -(d.x * g.nx + d.y * g.ny + d.z * g.nz);
@@ -256,7 +371,8 @@ __device__ __forceinline__ V3 hsl_roundtrip(V3 rgb)
 
 // ambient_occlusion, main.c:94-116: one cast, only distance/dst matters.
 template <bool COUNT>
-__device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const V3 n, Stream& st, Cnt& cnt)
+__device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const V3 n, double AO, Stream& st,
+                                            Cnt& cnt)
 {
     const V3 rd = random_dir<COUNT>(st, cnt);
     const V3 dir = normalize(n + rd);
@@ -269,24 +385,33 @@ __device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const
         const V3 df = hp - p;
         const double distance = sqrt(dot(df, df));
         double att = distance / t;
-        att = pm_pow(att, kp.AO);
+        att = pm_pow(att, AO);
         occ = occ + att;
     }
-    return (occ / 1.0) / kp.AO;
+    return (occ / 1.0) / AO;
 }
 
-// tracer, main.c:118-242.  The IOR stack (pile.h) is reduced to `top_n2`:
-// every translucent hit pushes (top.n2, m) (index_suivant_pile) and, when
-// exiting, pops that same pair again, so the stack only ever changes on
-// entry and only its top n2 is ever read (DESIGN.md "IOR stack").
+// tracer, main.c:118-242, adding its (radiance, albedo, normal) to the
+// accumulators.
+//
+// IOR stack (pile.h): every translucent hit pushes (top.n2, m)
+// (index_suivant_pile) and, when leaving, pops that same pair again, so the
+// stack only changes on entry and only its top n2 is ever read: one register.
+//
+// Albedo/normal (main.c:137-150,159): they are assigned only while
+// i == alpha_depth, i.e. along the primary chain of consecutive alpha holes,
+// and the next chain bounce always overwrites them; they are final when the
+// chain ends (first non-hole bounce, a miss, a light, or the last bounce).
 template <bool COUNT>
-__device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, Stream& st, V3& out_rad, V3& out_alb,
-                                      V3& out_nrm, Cnt& cnt)
+__device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, Stream& st, double* acc, Cnt& cnt)
 {
-    V3 inc = v3(0, 0, 0), rc = v3(1, 1, 1), alb = v3(0, 0, 0), nrm = v3(0, 0, 0);
-    bool is_alpha = false;
-    int alpha_depth = 0;
+    V3 inc = v3(0, 0, 0), rc = v3(1, 1, 1);
+    bool chain = true;
     double top_n2 = 1.0;
+    if (kp.B <= 0) {                                     // tracer returns (0, 0, 0) albedo/normal
+        acc_add(acc, 3, v3(0, 0, 0));
+        acc_add(acc, 6, v3(0, 0, 0));
+    }
     for (int i = 0; i < kp.B; i++) {
         double t;
         int idx;
@@ -305,28 +430,30 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, Stream& st,
             hn = normalize(v3(g.nx, g.ny, g.nz));
             mat = tri_material(kp, idx, hp, hn);
         }
-        if (i == 0) {
-            alb = mat.diff;
-            nrm = hn;
-        }
-        if (i == alpha_depth && is_alpha) {
-            alb = mat.es > 0 ? mat.emis : mat.diff;
-            nrm = hn;
-            is_alpha = false;
+        if (chain) {
+            // albedo/normal of this chain bounce are final unless it is an
+            // alpha hole with bounces left (then the next bounce overwrites)
+            if (kind != HIT_NONE && mat.es > 0) {        // direct view of a light, main.c:154-160
+                const V3 col = hsl_roundtrip(mat.emis);
+                acc_add(acc, 0, col);
+                acc_add(acc, 3, col);
+                acc_add(acc, 6, hn);
+                return;
+            }
+            if (!(kind != HIT_NONE && mat.alpha < 0.0001) || i == kp.B - 1) {
+                acc_add(acc, 3, mat.diff);
+                acc_add(acc, 6, hn);
+                chain = kind != HIT_NONE && mat.alpha < 0.0001;   // stays on only for a last-bounce hole
+            }
         }
         if (kind == HIT_NONE) break;
-        if (i == alpha_depth && mat.es > 0) {            // direct view of a light
-            const V3 col = hsl_roundtrip(mat.emis);
-            out_rad = col;
-            out_alb = col;
-            out_nrm = hn;
-            return;
-        }
         o = hp;
         const V3 diffuse_dir = normalize(hn + random_dir<COUNT>(st, cnt));
         const V3 reflected_dir = d - muls(hn, 2 * dot(d, hn));
         const V3 dr = diffuse_dir + muls(reflected_dir - diffuse_dir, mat.rs);
-        if (mat.alpha <= 0.99 && mat.alpha >= 0.0001) {  // refraction, main.c:167-193
+        if (mat.alpha < 0.0001) continue;                // alpha hole: pass through, main.c:200-206
+        chain = false;
+        if (mat.alpha <= 0.99) {                         // refraction, main.c:167-193 (alpha >= 1e-4 here)
             if (COUNT) cnt.c[RT_CNT_REFRACT] += 1;
             V3 nn = hn;
             double n1, n2;
@@ -346,22 +473,15 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, Stream& st,
                 continue;
             }
             d = dr;
-        }
-        if (mat.alpha > 0.99) {
-            is_alpha = false;
+        } else if (mat.alpha > 0.99) {
             d = dr;
         }
-        if (mat.alpha < 0.0001) {                        // alpha hole: pass through
-            is_alpha = true;
-            alpha_depth++;
-            continue;
-        }
         if (kp.useAO) {
-            const V3 em = muls(mat.emis, mat.es * 1.5 * kp.AO);
+            const V3 em = muls(mat.emis, mat.es * 1.5 * AO);
             inc = inc + mulv(em, rc);
             if (rc.x > 0.5 || rc.y > 0.5 || rc.z > 0.5) rc = mulv(mat.diff, muls(rc, 1.3));
             rc = mulv(mat.diff, rc);
-            const double occ = ao_factor<COUNT>(kp, hp, hn, st, cnt);
+            const double occ = ao_factor<COUNT>(kp, hp, hn, AO, st, cnt);
             rc = mulv(rc, v3(occ, occ, occ));
         } else {
             const V3 em = muls(mat.emis, mat.es);
@@ -370,9 +490,7 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, Stream& st,
             rc = mulv(mat.diff, rc);
         }
     }
-    out_rad = inc;
-    out_alb = alb;
-    out_nrm = nrm;
+    acc_add(acc, 0, inc);
 }
 
 // write_color_canva, rtutility.h:56-71 (sqrtf of the float-rounded product)
@@ -390,13 +508,24 @@ __device__ __forceinline__ void store3(double* base, long long i, V3 v)
     base[3 * i + 2] = v.z;
 }
 
-// fill_canva, main.c:245-284: one thread = one pixel, all S samples.
+__device__ __forceinline__ void write_pixel(const KParams& kp, long long li, V3 srad, V3 salb, V3 snrm)
+{
+    const double rapport = 1.0 / kp.S;
+    store3(kp.canva, li, v3(resolve(srad.x, rapport), resolve(srad.y, rapport), resolve(srad.z, rapport)));
+    const double S = (double)kp.S;
+    if (kp.albedo) store3(kp.albedo, li, divs(salb, S));
+    if (kp.normal) store3(kp.normal, li, divs(snrm, S));
+    if (kp.radiance) store3(kp.radiance, li, divs(srad, S));
+}
+
+// fill_canva, main.c:245-284: thread = (pixel, chunk of its samples).
 template <bool COUNT>
-__global__ __launch_bounds__(256) void render_kernel(const KParams kp)
+__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KParams kp)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
     const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int chunk = blockIdx.z;
     Cnt cnt;
     if (COUNT)
         for (int k = 0; k < RT_NCOUNTERS; ++k) cnt.c[k] = 0;
@@ -408,33 +537,35 @@ __global__ __launch_bounds__(256) void render_kernel(const KParams kp)
         valid = g < kp.row_end;
     }
     if (valid) {
-        const V3 co = v3(kp.cam_o[0], kp.cam_o[1], kp.cam_o[2]);
-        const V3 ch = v3(kp.cam_h[0], kp.cam_h[1], kp.cam_h[2]);
-        const V3 cv = v3(kp.cam_v[0], kp.cam_v[1], kp.cam_v[2]);
-        const V3 cc = v3(kp.cam_c[0], kp.cam_c[1], kp.cam_c[2]);
-        const double wm1 = (double)(kp.W - 1), hm1 = (double)(kp.H - 1);
         const uint32_t pixel = (uint32_t)g * (uint32_t)kp.W + (uint32_t)x;
-        V3 srad = v3(0, 0, 0), salb = v3(0, 0, 0), snrm = v3(0, 0, 0);
-        for (int s = 0; s < kp.S; ++s) {
+        const int s0 = (int)(((long long)chunk * kp.S) / kp.chunks);
+        const int s1 = (int)(((long long)(chunk + 1) * kp.S) / kp.chunks);
+        __shared__ double acc_lds[9 * 256];
+        double* acc = acc_lds + threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
+        for (int s = s0; s < s1; ++s) {
             Stream st;
             st.start(pixel, (uint32_t)s, kp.key0, kp.key1);
             const double ju = -0.5 + 1.0 * unit31(st.next31());     // randomDouble(-0.5, 0.5)
             const double jv = -0.5 + 1.0 * unit31(st.next31());
             const double jx = -0.5 + 1.0 * unit31(st.next31());
             const double jy = -0.5 + 1.0 * unit31(st.next31());
-            const double u = ((double)x + ju) / wm1;
-            const double v = ((double)g + jv) / hm1;
-            const double dx = jx * kp.ox, dy = jy * kp.oy;
+            const int b = opq0();
+            const cdptr U = (cdptr)kp.uni;
+            const double u = ((double)x + ju) / U[b + U_WM1];
+            const double v = ((double)g + jv) / U[b + U_HM1];
+            const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
             // get_ray, camera.h:42-55
+            const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
+            const V3 ch = v3(U[b + U_CAM_H], U[b + U_CAM_H + 1], U[b + U_CAM_H + 2]);
+            const V3 cv = v3(U[b + U_CAM_V], U[b + U_CAM_V + 1], U[b + U_CAM_V + 2]);
+            const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
             const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));
-            const V3 dest = co + muls(dir, kp.focus);
+            const V3 dest = co + muls(dir, U[b + U_FOCUS]);
             const V3 no = co + v3(dx, dy, 0);
             const V3 rd = normalize(dest - no);
-            V3 rad, alb, nrm;
-            trace<COUNT>(kp, no, rd, st, rad, alb, nrm, cnt);
-            srad = srad + rad;
-            salb = salb + alb;
-            snrm = snrm + nrm;
+            trace<COUNT>(kp, no, rd, U[b + U_AO], st, acc, cnt);
             if (COUNT) {
                 cnt.c[RT_CNT_SAMPLES] += 1;
                 cnt.c[RT_CNT_RNG_DRAWS] += st.n;
@@ -442,12 +573,17 @@ __global__ __launch_bounds__(256) void render_kernel(const KParams kp)
         }
         if (!COUNT) {
             const long long li = (long long)ly * kp.W + x;
-            const double rapport = 1.0 / kp.S;
-            store3(kp.canva, li, v3(resolve(srad.x, rapport), resolve(srad.y, rapport), resolve(srad.z, rapport)));
-            const double S = (double)kp.S;
-            if (kp.albedo) store3(kp.albedo, li, divs(salb, S));
-            if (kp.normal) store3(kp.normal, li, divs(snrm, S));
-            if (kp.radiance) store3(kp.radiance, li, divs(srad, S));
+            const V3 srad = v3(acc[0], acc[256], acc[512]);
+            const V3 salb = v3(acc[768], acc[1024], acc[1280]);
+            const V3 snrm = v3(acc[1536], acc[1792], acc[2048]);
+            if (kp.chunks == 1) {
+                write_pixel(kp, li, srad, salb, snrm);
+            } else {
+                double* p = kp.partial + ((long long)chunk * kp.local_rows * kp.W + li) * 9;
+                p[0] = srad.x; p[1] = srad.y; p[2] = srad.z;
+                p[3] = salb.x; p[4] = salb.y; p[5] = salb.z;
+                p[6] = snrm.x; p[7] = snrm.y; p[8] = snrm.z;
+            }
         }
     }
     if (COUNT) {
@@ -456,6 +592,29 @@ __global__ __launch_bounds__(256) void render_kernel(const KParams kp)
             for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
             if (lane == 0 && v) atomicAdd(kp.counters + k, v);
         }
+    }
+}
+
+// Sum the chunk partials of each pixel in chunk order, then resolve.
+__global__ __launch_bounds__(256) void combine_kernel(const KParams kp)
+{
+    const long long npx = (long long)kp.local_rows * kp.W;
+    for (long long li = (long long)blockIdx.x * blockDim.x + threadIdx.x; li < npx;
+         li += (long long)gridDim.x * blockDim.x) {
+        const int ly = (int)(li / kp.W);
+        const int lt = ly / kp.tile_rows, yy = ly - lt * kp.tile_rows;
+        const int g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + yy;
+        if (g >= kp.row_end) continue;
+        const double* p = kp.partial + li * 9;
+        double a[9];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) a[j] = p[j];
+        for (int c = 1; c < kp.chunks; ++c) {
+            const double* q = kp.partial + ((long long)c * npx + li) * 9;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) a[j] = a[j] + q[j];
+        }
+        write_pixel(kp, li, v3(a[0], a[1], a[2]), v3(a[3], a[4], a[5]), v3(a[6], a[7], a[8]));
     }
 }
 
@@ -475,6 +634,20 @@ __global__ __launch_bounds__(256) void assemble_kernel(const double* __restrict_
         const long long src = (long long)r * rank_stride + ((long long)lt * tile_rows + y) * W + i;
         out[e] = gathered[src * 3 + c];
     }
+}
+
+// Per-launch uniform block: the values travel as this kernel's by-value
+// argument (captured at enqueue), so the copy is stream-ordered without a
+// pageable host staging buffer.
+__global__ void set_uniforms_kernel(const UniBlock u, double* __restrict__ dst)
+{
+    if (threadIdx.x < U_COUNT) dst[threadIdx.x] = u.v[threadIdx.x];
+}
+
+int launch_set_uniforms(const UniBlock& u, double* d_uni, void* stream)
+{
+    hipLaunchKernelGGL(set_uniforms_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, u, d_uni);
+    return (int)hipGetLastError();
 }
 
 // Device-math self test (rt_selftest_math).
@@ -502,7 +675,7 @@ __global__ void selftest_kernel(int op, const double* __restrict__ in, double* _
     case 6: out[i] = (double)sqrtf((float)in[i]); break;
     case 7: {
         const double* q = in + 6 * i;
-        const Philox p = philox4x32_10((uint32_t)q[0], (uint32_t)q[1], (uint32_t)q[2], (uint32_t)q[3],
+        const Philox p = philox4x32_10<false>((uint32_t)q[0], (uint32_t)q[1], (uint32_t)q[2], (uint32_t)q[3],
                                        (uint32_t)q[4], (uint32_t)q[5]);
         out[4 * i + 0] = p.w0;
         out[4 * i + 1] = p.w1;
@@ -514,25 +687,26 @@ __global__ void selftest_kernel(int op, const double* __restrict__ in, double* _
     }
 }
 
-static int grid_for(const KParams& kp, dim3& grid)
+static dim3 grid_for(const KParams& kp)
 {
-    grid = dim3((unsigned)((kp.W + 15) / 16), (unsigned)((kp.local_rows + 15) / 16), 1);
-    return 0;
+    return dim3((unsigned)((kp.W + 15) / 16), (unsigned)((kp.local_rows + 15) / 16), (unsigned)kp.chunks);
 }
 
 int launch_render(const KParams& kp, void* stream)
 {
-    dim3 grid;
-    grid_for(kp, grid);
-    hipLaunchKernelGGL(render_kernel<false>, grid, dim3(256), 0, (hipStream_t)stream, kp);
+    hipLaunchKernelGGL(render_kernel<false>, grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
+    if (kp.chunks > 1) {
+        const long long npx = (long long)kp.local_rows * kp.W;
+        long long blocks = (npx + 255) / 256;
+        if (blocks > 8192) blocks = 8192;
+        hipLaunchKernelGGL(combine_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, kp);
+    }
     return (int)hipGetLastError();
 }
 
 int launch_count(const KParams& kp, void* stream)
 {
-    dim3 grid;
-    grid_for(kp, grid);
-    hipLaunchKernelGGL(render_kernel<true>, grid, dim3(256), 0, (hipStream_t)stream, kp);
+    hipLaunchKernelGGL(render_kernel<true>, grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
     return (int)hipGetLastError();
 }
 

@@ -14,7 +14,7 @@ from .types import (Vec3, Ray, Material, Sphere, UV, Triangle, Camera, ThreadDat
                     RT_RNG_PHILOX, RT_RNG_GLIBC, RT_NCOUNTERS, COUNTER_NAMES)
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "librt_hip.so")
+LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(PKG_DIR, "librt_hip.so")   # override: A/B builds
 HOST_LIB_PATH = os.path.join(PKG_DIR, "librt_host.so")
 
 
@@ -112,7 +112,7 @@ def make_scene(spheres=None, triangles=None, quel_mat=None, mat_list=None, tex_w
 
 
 def make_params(W, H, spp, bounces, cam, focus=3.0, aperture=(0.0, 0.0), use_ao=False, ao=2.5,
-                seed=1010, rng=RT_RNG_PHILOX, compat=1):
+                seed=1010, rng=RT_RNG_PHILOX, compat=1, chunks=1):
     p = Params()
     p.largeur_image, p.hauteur_image = W, H
     p.nbRayonParPixel, p.nbRebondMax = spp, bounces
@@ -122,6 +122,7 @@ def make_params(W, H, spp, bounces, cam, focus=3.0, aperture=(0.0, 0.0), use_ao=
     p.useAO, p.AO_intensity = int(bool(use_ao)), ao
     p.compat_int_truncation = compat
     p.rng, p.seed = rng, seed
+    p.spp_chunks = chunks
     return p
 
 

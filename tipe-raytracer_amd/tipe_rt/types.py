@@ -89,7 +89,7 @@ class Params(C.Structure):
                 ("ouverture_x", C.c_double), ("ouverture_y", C.c_double),
                 ("AO_intensity", C.c_double), ("useAO", C.c_int),
                 ("compat_int_truncation", C.c_int), ("rng", C.c_int),
-                ("reserved0", C.c_int), ("seed", C.c_ulonglong)]
+                ("spp_chunks", C.c_int), ("seed", C.c_ulonglong)]
 
 
 class Tiling(C.Structure):
