@@ -1,0 +1,136 @@
+"""C-ABI boundary (no GPU needed): the libraries load, export every entry
+point their headers declare, the reference-shaped structs have the
+reference's x86-64 layout, and argument validation fails loudly before any
+device work."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+import tipe_rt
+from tipe_rt import types as T
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INC = os.path.join(ROOT, "include", "rt")
+
+
+def declared(header):
+    src = open(os.path.join(INC, header)).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", src)) - {"rt_version_t"})
+
+
+def exported(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def test_rt_h_symbols_exported():
+    syms = exported(tipe_rt.LIB_PATH)
+    missing = [s for s in declared("rt.h") if s not in syms]
+    assert not missing, missing
+    assert set(tipe_rt.EXPORTED_SYMBOLS) <= syms
+
+
+def test_host_h_symbols_exported():
+    syms = exported(tipe_rt.HOST_LIB_PATH)
+    missing = [s for s in declared("host.h") if s not in syms]
+    assert not missing, missing
+
+
+def test_library_loads_and_reports_version():
+    L = tipe_rt.lib()
+    assert b"gfx950" in L.rt_version()
+    p = T.Params()
+    L.rt_params_init(C.byref(p))
+    assert p.rng == T.RT_RNG_PHILOX and p.seed == 1010 and p.compat_int_truncation == 1 and p.spp_chunks == 1
+
+
+LAYOUT_C = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "rt/rt.h"
+#define P(t) printf(#t " %zu\n", sizeof(t))
+#define O(t, f) printf(#t "." #f " %zu\n", offsetof(t, f))
+int main(void) {
+  P(rt_vec3); P(rt_material); P(rt_sphere); P(rt_triangle); P(rt_camera); P(rt_thread_data);
+  P(rt_scene); P(rt_params); P(rt_tiling); P(rt_frame);
+  O(rt_material, alpha); O(rt_triangle, uvB); O(rt_thread_data, nbRayonParPixel);
+  O(rt_thread_data, triangle_list); O(rt_thread_data, AO_intensity); O(rt_scene, quelMatPourTri);
+  O(rt_params, cam); O(rt_params, focus_distance); O(rt_params, rng); O(rt_params, spp_chunks);
+  O(rt_params, seed); O(rt_frame, radiance);
+  return 0;
+}
+"""
+
+
+def test_struct_layouts_match_ctypes_mirror(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(LAYOUT_C)
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                               check=True).stdout.splitlines())
+    got = {k: int(v) for k, v in got.items()}
+    mirror = {"rt_vec3": T.Vec3, "rt_material": T.Material, "rt_sphere": T.Sphere, "rt_triangle": T.Triangle,
+              "rt_camera": T.Camera, "rt_thread_data": T.ThreadData, "rt_scene": T.Scene, "rt_params": T.Params,
+              "rt_tiling": T.Tiling, "rt_frame": T.Frame}
+    for name, cls in mirror.items():
+        assert got[name] == C.sizeof(cls), name
+    for key, val in got.items():
+        if "." in key:
+            t, f = key.split(".")
+            assert getattr(mirror[t], f).offset == val, key
+    # the reference's own sizes
+    assert (got["rt_material"], got["rt_sphere"], got["rt_triangle"], got["rt_camera"],
+            got["rt_thread_data"]) == (80, 112, 200, 96, 248)
+
+
+def test_validation_errors_without_device():
+    L = tipe_rt.lib()
+    sc = T.Scene()
+    p = T.Params()
+    L.rt_params_init(C.byref(p))
+    p.largeur_image, p.hauteur_image, p.nbRayonParPixel, p.nbRebondMax = 8, 6, 1, 5
+    buf = (C.c_double * (8 * 6 * 3))()
+    assert L.rt_render_rows(None, C.byref(p), 5, 0, buf, None, None) == T.RT_EINVAL
+    assert L.rt_render_rows(C.byref(sc), C.byref(p), 6, 0, buf, None, None) == T.RT_EINVAL   # row out of range
+    p.nbRayonParPixel = 0
+    assert L.rt_render_rows(C.byref(sc), C.byref(p), 5, 0, buf, None, None) == T.RT_EINVAL
+    assert b"nbRayonParPixel" in L.rt_last_error()
+    p.nbRayonParPixel = 1
+    p.rng = T.RT_RNG_GLIBC
+    assert L.rt_render_rows(C.byref(sc), C.byref(p), 5, 0, buf, None, None) == T.RT_EUNSUPPORTED
+    sc.nbTriangles = 1                    # triangles without arrays
+    p.rng = T.RT_RNG_PHILOX
+    assert L.rt_render_rows(C.byref(sc), C.byref(p), 5, 0, buf, None, None) == T.RT_EINVAL
+    assert L.rt_assemble_async(None, 0, 1, 1, 1, 1, 1, None, None) == T.RT_EINVAL
+    assert L.rt_selftest_math(9, buf, buf, 1) == T.RT_EINVAL
+
+
+def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
+    """The Python mirror refuses to run without librt_hip.so."""
+    import importlib
+    monkeypatch.setenv("RT_HIP_LIB", str(tmp_path / "nope.so"))
+    mod = importlib.reload(tipe_rt)
+    try:
+        mod._lib = None
+        with pytest.raises(RuntimeError, match="no CPU fallback"):
+            mod.lib()
+    finally:
+        monkeypatch.delenv("RT_HIP_LIB")
+        importlib.reload(tipe_rt)
+
+
+def test_kernel_resource_usage_builds_for_gfx950():
+    """The HIP sources cross-compile for gfx950 with no VGPR spills above
+    the budget recorded in DESIGN.md (build check, no GPU)."""
+    out = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tipe-raytracer_amd"), "resource-usage"],
+                         capture_output=True, text=True)
+    txt = out.stdout + out.stderr
+    m = re.search(r"render_kernelILb0.*?VGPRs: (\d+).*?VGPRs Spill: (\d+)", txt, re.S)
+    assert m, txt[-2000:]
+    vgprs, spills = int(m.group(1)), int(m.group(2))
+    assert vgprs <= 128 and spills <= 32
