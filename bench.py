@@ -45,7 +45,7 @@ HBM_PEAK_GBS = 8000.0
 
 def flops_per_launch(cnt, ns, nt):
     """F = 40 + C(25 Ns + 40 Nt + 18) + 5 D + 100 Bn + 80 T + 40 R per sample."""
-    s, casts, disc, shade, tex, refr = (cnt[i] for i in (0, 1, 3, 5, 6, 7))
+    s, casts, disc, shade, tex, refr = (cnt[i] for i in (0, 1, 3, 5, 6, 7))   # rt.h RT_CNT_*
     return 40 * s + casts * (25 * ns + 40 * nt + 18) + 5 * disc + 100 * shade + 80 * tex + 40 * refr
 
 

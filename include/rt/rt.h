@@ -159,6 +159,8 @@ enum {
     RT_CNT_TEX_HITS,      /* closest hits on a triangle (texel fetch)      */
     RT_CNT_REFRACT,       /* refraction-branch events                      */
     RT_CNT_RNG_DRAWS,     /* 31-bit draws consumed                         */
+    RT_CNT_EXACT_RESCANS, /* sphere scans redone exactly (candidate pass
+                             ambiguous; GPU diagnostic, the oracle reports 0) */
     RT_NCOUNTERS
 };
 /* Same traversal as rt_render_async, no frame; adds event counts into the

@@ -167,7 +167,9 @@ def test_counters_match_oracle():
     torch.cuda.synchronize()
     got = d_cnt.cpu().numpy().astype(np.uint64)
     ds.close()
-    assert list(got) == list(ref), dict(zip(tipe_rt.COUNTER_NAMES, zip(got, ref)))
+    k = tipe_rt.types.RT_CNT_EXACT_RESCANS           # GPU-only diagnostic
+    assert list(got[:k]) == list(ref[:k]), dict(zip(tipe_rt.COUNTER_NAMES, zip(got, ref)))
+    assert got[k] <= got[tipe_rt.types.RT_CNT_CASTS] // 1000   # candidate pass almost never ambiguous
 
 
 # ---- boundary behaviour --------------------------------------------------------

@@ -144,34 +144,34 @@ __device__ __forceinline__ double pm_acos_R(int b, double z)
 
 __device__ __forceinline__ double pm_acos(double x)
 {
+    // fdlibm's three cases evaluated branch-free: every lane performs exactly
+    // the operations of its own case (same values as the branchy form in
+    // oracle/pm_math.h), but the wave runs one rational R(z), one sqrt and
+    // one extra division instead of three divergent copies of them.
     const int b = opq0();
     const double PIO2_HI = KCV(b, KC_PIO2_HI), PIO2_LO = KCV(b, KC_PIO2_LO), PI = KCV(b, KC_PI);
     const unsigned long long u = (unsigned long long)__double_as_longlong(x);
     const uint32_t hx = (uint32_t)(u >> 32);
     const uint32_t ix = hx & 0x7fffffffu;
-    if (ix >= 0x3ff00000u) {
-        if (((ix - 0x3ff00000u) | (uint32_t)u) == 0u) return (hx >> 31) ? PI + 2.0 * PIO2_LO : 0.0;
-        return (x - x) / (x - x);
-    }
-    if (ix < 0x3fe00000u) {
-        if (ix <= 0x3c600000u) return PIO2_HI + PIO2_LO;
-        const double r = pm_acos_R(b, x * x);
-        return PIO2_HI - (x - (PIO2_LO - x * r));
-    }
-    if (hx >> 31) {
-        const double z = (1.0 + x) * 0.5;
-        const double r = pm_acos_R(b, z);
-        const double s = sqrt(z);
-        const double w = r * s - PIO2_LO;
-        return PI - 2.0 * (s + w);
-    }
-    const double z = (1.0 - x) * 0.5;
+    const bool small = ix < 0x3fe00000u;          // |x| < 0.5
+    const bool neg = (hx >> 31) != 0;
+    const double z = small ? x * x : (neg ? (1.0 + x) * 0.5 : (1.0 - x) * 0.5);
+    const double r = pm_acos_R(b, z);
     const double s = sqrt(z);
+    // x >= 0.5
     const double df = __longlong_as_double((long long)((unsigned long long)__double_as_longlong(s) & 0xffffffff00000000ull));
     const double c = (z - df * df) / (s + df);
-    const double r = pm_acos_R(b, z);
-    const double w = r * s + c;
-    return 2.0 * (df + w);
+    const double res_pos = 2.0 * (df + (r * s + c));
+    // x <= -0.5
+    const double res_neg = PI - 2.0 * (s + (r * s - PIO2_LO));
+    // |x| < 0.5
+    const double res_small = (ix <= 0x3c600000u) ? PIO2_HI + PIO2_LO : PIO2_HI - (x - (PIO2_LO - x * r));
+    double res = small ? res_small : (neg ? res_neg : res_pos);
+    if (ix >= 0x3ff00000u) {                       // |x| >= 1 or NaN (x == -1 only, in the sampler)
+        if (((ix - 0x3ff00000u) | (uint32_t)u) == 0u) res = neg ? PI + 2.0 * PIO2_LO : 0.0;
+        else res = (x - x) / (x - x);
+    }
+    return res;
 }
 
 // ---- pow ---------------------------------------------------------------------

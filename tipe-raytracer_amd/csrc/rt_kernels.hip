@@ -201,6 +201,7 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
         else amb = true;     // cannot happen within the bound; stay exact anyway
     }
     if (amb) {               // exact reference scan for this ray
+        if (COUNT) cnt.c[RT_CNT_EXACT_RESCANS] += 1;
         t = INF;
         win = -1;
         for (int k = 0; k < kp.ns_pad; ++k) {

@@ -7,9 +7,9 @@ RT_RNG_PHILOX, RT_RNG_GLIBC = 0, 1
 
 (RT_CNT_SAMPLES, RT_CNT_CASTS, RT_CNT_SPHERE_TESTS, RT_CNT_SPHERE_DISC,
  RT_CNT_TRI_TESTS, RT_CNT_SHADE, RT_CNT_TEX_HITS, RT_CNT_REFRACT,
- RT_CNT_RNG_DRAWS, RT_NCOUNTERS) = range(10)
+ RT_CNT_RNG_DRAWS, RT_CNT_EXACT_RESCANS, RT_NCOUNTERS) = range(11)
 COUNTER_NAMES = ["samples", "casts", "sphere_tests", "sphere_disc", "tri_tests",
-                 "shade", "tex_hits", "refract", "rng_draws"]
+                 "shade", "tex_hits", "refract", "rng_draws", "exact_rescans"]
 
 
 class Vec3(C.Structure):
