@@ -172,8 +172,8 @@ int rt_count_async(const rt_device_scene* scene, const rt_params* params,
 /* Device-math self test: evaluates one device primitive on n host inputs
  * (synchronous, device 0).  op: 0 acos, 1 sinf, 2 cosf, 3 pow(x, y),
  * 4 sqrt, 5 x/y, 6 sqrtf, 7 philox word (in[0..3] = ctr, in[4..5] = key as
- * integers in doubles; returns 4 words per input).  Inputs are read as pairs
- * (x, y) for binary ops. */
+ * integers in doubles; returns 4 words per input), 8 normalize (3 doubles in,
+ * 3 out, vec3.h:137-139).  Inputs are read as pairs (x, y) for binary ops. */
 int rt_selftest_math(int op, const double* in, double* out, int n);
 
 #ifdef __cplusplus

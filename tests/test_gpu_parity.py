@@ -89,6 +89,25 @@ def test_device_math_bitexact():
     assert (tipe_rt.selftest_math(6, fs.astype(np.float64), n) == np.sqrt(fs).astype(np.float64)).all()
 
 
+def test_device_normalize_fast_path_is_ieee():
+    """normalize() skips the sqrt/division range fixups on in-range lanes and
+    shares 1/|a| (rt_kernels.hip); it must equal a / sqrt(a.a) in IEEE f64
+    for every input, including the lanes routed to the generic path."""
+    rng = np.random.default_rng(11)
+    n = 1 << 18
+    v = rng.normal(size=(n, 3)) * rng.choice([1e-300, 1e-200, 1e-9, 1.0, 1e3, 1e200, 1e300], (n, 1))
+    v[: n // 16, rng.integers(0, 3)] = 0.0                      # zero components
+    v[n // 16: n // 8, 1] *= 1e-290                             # one tiny component
+    v[n // 8: n // 8 + 64] = [[-0.0, 1.0, 0.0]]
+    v[n // 8 + 64: n // 8 + 128] = rng.normal(size=(64, 3)) * 2.0 ** -380
+    got = tipe_rt.selftest_math(8, v.ravel(), n).reshape(n, 3)
+    with np.errstate(all="ignore"):
+        L = np.sqrt((v[:, 0] * v[:, 0] + v[:, 1] * v[:, 1]) + v[:, 2] * v[:, 2])
+        want = v / L[:, None]
+    same = (got.view(np.uint64) == want.view(np.uint64)) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), v[~same.all(1)][:4]
+
+
 def test_device_philox_matches_oracle():
     o = oracle_ffi.oracle()
     rng = np.random.default_rng(3)

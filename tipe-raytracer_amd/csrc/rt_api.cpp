@@ -573,7 +573,7 @@ void* rt_fill_canva(void* arg)
 
 int rt_selftest_math(int op, const double* in, double* out, int n)
 {
-    if (!in || !out || n < 0 || op < 0 || op > 7) return fail(RT_EINVAL, "bad selftest arguments");
+    if (!in || !out || n < 0 || op < 0 || op > 8) return fail(RT_EINVAL, "bad selftest arguments");
     if (n == 0) return RT_OK;
     int dev = 0;
     {
@@ -583,8 +583,8 @@ int rt_selftest_math(int op, const double* in, double* out, int n)
         dev = g_devices[0];
     }
     DeviceGuard guard(dev);
-    const size_t nin = (size_t)n * (op == 7 ? 6 : (op == 3 || op == 5) ? 2 : 1);
-    const size_t nout = (size_t)n * (op == 7 ? 4 : 1);
+    const size_t nin = (size_t)n * (op == 7 ? 6 : op == 8 ? 3 : (op == 3 || op == 5) ? 2 : 1);
+    const size_t nout = (size_t)n * (op == 7 ? 4 : op == 8 ? 3 : 1);
     double *d_in = nullptr, *d_out = nullptr;
     HIP_TRY(hipMalloc((void**)&d_in, nin * sizeof(double)));
     hipError_t e = hipMalloc((void**)&d_out, nout * sizeof(double));

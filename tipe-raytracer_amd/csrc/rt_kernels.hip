@@ -65,7 +65,37 @@ __device__ __forceinline__ V3 cross(V3 u, V3 v)
 {
     return v3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
 }
-__device__ __forceinline__ V3 normalize(V3 a) { return divs(a, sqrt(dot(a, a))); }   // vec3.h:137-139
+
+// normalize(a) = a / sqrt(dot(a, a)), vec3.h:137-139, bit-exact.  The fast
+// branch runs the compiler's own gfx950 lowerings of the IEEE f64 sqrt
+// (v_rsq + Goldschmidt/Newton, 10 ops) and division (v_div_scale, v_rcp, two
+// Newton steps, mul, fma, v_div_fmas, v_div_fixup) without their range
+// scaling and special-value fixups, and shares the refined reciprocal of the
+// length among the three quotients (it depends only on the divisor).  Those
+// fixups are identities when dot(a,a) is in [2^-760, 2^760] and no component
+// is below 2^-900 in magnitude (no scaling, no zero/inf/denormal operand or
+// intermediate); other lanes -- zero components, NaN, extreme lengths -- take
+// the generic `/` and `sqrt`.  rt_selftest_math op 8 checks the two agree.
+__device__ __forceinline__ V3 normalize(V3 a)
+{
+    const double n2 = dot(a, a);
+    const double mn = fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
+    if (n2 >= 0x1p-760 && n2 <= 0x1p760 && mn >= 0x1p-900) {
+        const double y = __builtin_amdgcn_rsq(n2);
+        double g = n2 * y, h = y * 0.5;
+        const double r = fma(-h, g, 0.5);
+        g = fma(g, r, g);
+        h = fma(h, r, h);
+        g = fma(fma(-g, g, n2), h, g);
+        const double L = fma(fma(-g, g, n2), h, g);           // == sqrt(n2)
+        double rc = __builtin_amdgcn_rcp(L);
+        rc = fma(rc, fma(-L, rc, 1.0), rc);
+        rc = fma(rc, fma(-L, rc, 1.0), rc);
+        const double qx = a.x * rc, qy = a.y * rc, qz = a.z * rc;
+        return v3(fma(fma(-L, qx, a.x), rc, qx), fma(fma(-L, qy, a.y), rc, qy), fma(fma(-L, qz, a.z), rc, qz));
+    }
+    return divs(a, sqrt(n2));
+}
 
 struct Mat {
     V3 diff, emis;
@@ -682,6 +712,13 @@ __global__ void selftest_kernel(int op, const double* __restrict__ in, double* _
         out[4 * i + 1] = p.w1;
         out[4 * i + 2] = p.w2;
         out[4 * i + 3] = p.w3;
+        break;
+    }
+    case 8: {                                   // normalize (fast lanes and generic lanes)
+        const V3 v = normalize(v3(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
+        out[3 * i + 0] = v.x;
+        out[3 * i + 1] = v.y;
+        out[3 * i + 2] = v.z;
         break;
     }
     default: out[i] = 0.0;

@@ -188,6 +188,6 @@ def assemble_async(gathered_ptr, world, tile_rows, rows_per_rank, W, H, out_ptr,
 
 def selftest_math(op, inputs, n):
     inp = np.ascontiguousarray(inputs, dtype=np.float64)
-    out = np.zeros(n * (4 if op == 7 else 1))
+    out = np.zeros(n * (4 if op == 7 else 3 if op == 8 else 1))
     check(lib().rt_selftest_math(op, inp.ctypes.data, out.ctypes.data, n))
     return out
