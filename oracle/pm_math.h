@@ -2,8 +2,9 @@
  * oracle/pm_math.h — TEST INFRASTRUCTURE (CPU oracle only; never shipped).
  *
  * "Portable math": the transcendental functions of the RT_RNG_PHILOX stream
- * spec, written with IEEE-754 double +,-,*,/,sqrt and exact conversions only
- * (no FMA, no libm), so that the oracle and the HIP kernel — two independent
+ * spec, written with IEEE-754 double +,-,*,/,sqrt, fma (one rounding: C99
+ * fma() here, v_fma_f64 on the device) and exact conversions only (no libm
+ * transcendentals), so that the oracle and the HIP kernel — two independent
  * restatements of DESIGN.md §"Portable math" — agree bit for bit.
  *
  * They stand in for the libm calls the reference makes on the sampling path:
@@ -25,32 +26,32 @@ static inline uint64_t pm_bits(double x) { uint64_t u; memcpy(&u, &x, 8); return
 static inline double pm_from_bits(uint64_t u) { double x; memcpy(&x, &u, 8); return x; }
 
 /* ---- sin/cos of a float argument, evaluated in double, rounded to float -- */
-/* Cody-Waite reduction by pi/2 in three 33-bit pieces, Taylor polynomials to
- * degree 17 (sin) / 16 (cos) on |r| <= pi/4. */
+/* Cody-Waite reduction by pi/2 (33-bit head, exact with FMA, plus tail) and
+ * the fdlibm minimax kernels (__kernel_sin degree 13, __kernel_cos degree 14)
+ * in FMA Horner form on |r| <= pi/4.  The float results are the correctly
+ * rounded sin/cos for every float in [0, 2*pi] (exhaustively checked against
+ * sinl/cosl, DESIGN.md "Portable math"); the domain used is [0, 2*pi]. */
 static const double PM_TWO_OVER_PI = 0x1.45f306dc9c883p-1;
 static const double PM_PIO2_1 = 0x1.921fb54400000p+0;
-static const double PM_PIO2_2 = 0x1.0b4611a600000p-34;
-static const double PM_PIO2_3 = 0x1.3198a2e000000p-69;
-static const double PM_S1 = -0x1.5555555555555p-3, PM_S2 = 0x1.1111111111111p-7,
-                    PM_S3 = -0x1.a01a01a01a01ap-13, PM_S4 = 0x1.71de3a556c734p-19,
-                    PM_S5 = -0x1.ae64567f544e4p-26, PM_S6 = 0x1.6124613a86d09p-33,
-                    PM_S7 = -0x1.ae7f3e733b81fp-41, PM_S8 = 0x1.952c77030ad4ap-49;
-static const double PM_C1 = -0x1.0000000000000p-1, PM_C2 = 0x1.5555555555555p-5,
-                    PM_C3 = -0x1.6c16c16c16c17p-10, PM_C4 = 0x1.a01a01a01a01ap-16,
-                    PM_C5 = -0x1.27e4fb7789f5cp-22, PM_C6 = 0x1.1eed8eff8d898p-29,
-                    PM_C7 = -0x1.93974a8c07c9dp-37, PM_C8 = 0x1.ae7f3e733b81fp-45;
+static const double PM_PIO2_1T = 0x1.0b4611a626331p-34;
+static const double PM_S1 = -0x1.5555555555549p-3, PM_S2 = 0x1.111111110f8a6p-7,
+                    PM_S3 = -0x1.a01a019c161d5p-13, PM_S4 = 0x1.71de357b1fe7dp-19,
+                    PM_S5 = -0x1.ae5e68a2b9cebp-26, PM_S6 = 0x1.5d93a5acfd57cp-33;
+static const double PM_C1 = 0x1.555555555554cp-5, PM_C2 = -0x1.6c16c16c15177p-10,
+                    PM_C3 = 0x1.a01a019cb1590p-16, PM_C4 = -0x1.27e4f809c52adp-22,
+                    PM_C5 = 0x1.1ee9ebdb4b1c4p-29, PM_C6 = -0x1.8fae9be8838d4p-37;
 
 /* returns quadrant q in [0,3]; *s = sin(r), *c = cos(r) */
 static inline int pm_reduce_sincos(float x, double* s, double* c)
 {
     double xd = (double)x;
     double kd = nearbyint(xd * PM_TWO_OVER_PI);          /* round half even */
-    double r = ((xd - kd * PM_PIO2_1) - kd * PM_PIO2_2) - kd * PM_PIO2_3;
+    double r = fma(-kd, PM_PIO2_1T, fma(-kd, PM_PIO2_1, xd));
     double z = r * r;
-    double ps = PM_S1 + z * (PM_S2 + z * (PM_S3 + z * (PM_S4 + z * (PM_S5 + z * (PM_S6 + z * (PM_S7 + z * PM_S8))))));
-    double pc = PM_C1 + z * (PM_C2 + z * (PM_C3 + z * (PM_C4 + z * (PM_C5 + z * (PM_C6 + z * (PM_C7 + z * PM_C8))))));
-    *s = r + (r * z) * ps;
-    *c = 1.0 + z * pc;
+    double ps = fma(z, fma(z, fma(z, fma(z, fma(z, PM_S6, PM_S5), PM_S4), PM_S3), PM_S2), PM_S1);
+    double pc = fma(z, fma(z, fma(z, fma(z, fma(z, PM_C6, PM_C5), PM_C4), PM_C3), PM_C2), PM_C1);
+    *s = fma(r * z, ps, r);
+    *c = fma(z * z, pc, fma(-0.5, z, 1.0));
     return (int)((int64_t)kd & 3);
 }
 
@@ -70,7 +71,7 @@ static inline float pm_cosf(float x)
     return (float)v;
 }
 
-/* ---- acos: the classic fdlibm rational scheme (< 1 ulp) ---------------- */
+/* ---- acos: the classic fdlibm rational scheme (< 1 ulp), FMA Horner ------ */
 static const double PM_PIO2_HI = 0x1.921fb54442d18p+0, PM_PIO2_LO = 0x1.1a62633145c07p-54,
                     PM_PI = 0x1.921fb54442d18p+1;
 static const double PM_PS0 = 0x1.5555555555555p-3, PM_PS1 = -0x1.4d61203eb6f7dp-2,
@@ -81,8 +82,8 @@ static const double PM_QS1 = -0x1.33a271c8a2d4bp+1, PM_QS2 = 0x1.02ae59c598ac8p+
 
 static inline double pm_acos_R(double z)
 {
-    double p = z * (PM_PS0 + z * (PM_PS1 + z * (PM_PS2 + z * (PM_PS3 + z * (PM_PS4 + z * PM_PS5)))));
-    double q = 1.0 + z * (PM_QS1 + z * (PM_QS2 + z * (PM_QS3 + z * PM_QS4)));
+    double p = z * fma(z, fma(z, fma(z, fma(z, fma(z, PM_PS5, PM_PS4), PM_PS3), PM_PS2), PM_PS1), PM_PS0);
+    double q = fma(z, fma(z, fma(z, fma(z, PM_QS4, PM_QS3), PM_QS2), PM_QS1), 1.0);
     return p / q;
 }
 
@@ -99,22 +100,22 @@ static inline double pm_acos(double x)
     if (ix < 0x3fe00000u) {                        /* |x| < 0.5 */
         if (ix <= 0x3c600000u) return PM_PIO2_HI + PM_PIO2_LO;
         double r = pm_acos_R(x * x);
-        return PM_PIO2_HI - (x - (PM_PIO2_LO - x * r));
+        return PM_PIO2_HI - (x - fma(-x, r, PM_PIO2_LO));
     }
     if (hx >> 31) {                                /* x <= -0.5 */
         double z = (1.0 + x) * 0.5;
         double r = pm_acos_R(z);
         double s = sqrt(z);
-        double w = r * s - PM_PIO2_LO;
+        double w = fma(r, s, -PM_PIO2_LO);
         return PM_PI - 2.0 * (s + w);
     }
     {                                              /* x >= 0.5 */
         double z = (1.0 - x) * 0.5;
         double s = sqrt(z);
         double df = pm_from_bits(pm_bits(s) & 0xffffffff00000000ull);
-        double c = (z - df * df) / (s + df);
+        double c = fma(-df, df, z) / (s + df);
         double r = pm_acos_R(z);
-        double w = r * s + c;
+        double w = fma(r, s, c);
         return 2.0 * (df + w);
     }
 }

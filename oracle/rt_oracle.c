@@ -806,6 +806,53 @@ void oracle_scan_sincosf(float lo, float hi, int nthreads, unsigned long long* n
     free(th);
 }
 
+/* pm_sinf/pm_cosf against the correctly rounded float sin/cos: the x87
+ * long-double sinl/cosl, rounded to float (64-bit significand; a double
+ * rounding through it would need a sin value within 2^-64 relative of a
+ * float midpoint). */
+static void* sincos_cr_worker(void* arg)
+{
+    scan_job* j = (scan_job*)arg;
+    for (long long b = j->k0; b < j->k1; b += j->step) {
+        const uint32_t bits = (uint32_t)b;
+        float x;
+        memcpy(&x, &bits, 4);
+        const float s1 = (float)sinl((long double)x), c1 = (float)cosl((long double)x);
+        const float s2 = pm_sinf(x), c2 = pm_cosf(x);
+        j->tot++;
+        if (memcmp(&s1, &s2, 4)) j->d1++;
+        if (memcmp(&c1, &c2, 4)) j->d2++;
+    }
+    return NULL;
+}
+
+void oracle_scan_sincosf_cr(float lo, float hi, long long step, int nthreads, unsigned long long* n_total,
+                            unsigned long long* n_sin_diff, unsigned long long* n_cos_diff)
+{
+    uint32_t b0, b1;
+    memcpy(&b0, &lo, 4);
+    memcpy(&b1, &hi, 4);
+    if (nthreads < 1) nthreads = 1;
+    if (step < 1) step = 1;
+    scan_job* jobs = (scan_job*)calloc((size_t)nthreads, sizeof(scan_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t].k0 = (long long)b0 + t * step;
+        jobs[t].k1 = (long long)b1 + 1;
+        jobs[t].step = step * nthreads;
+        pthread_create(&th[t], NULL, sincos_cr_worker, &jobs[t]);
+    }
+    *n_total = *n_sin_diff = *n_cos_diff = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        *n_total += jobs[t].tot;
+        *n_sin_diff += jobs[t].d1;
+        *n_cos_diff += jobs[t].d2;
+    }
+    free(jobs);
+    free(th);
+}
+
 static void* acos_worker(void* arg)
 {
     scan_job* j = (scan_job*)arg;

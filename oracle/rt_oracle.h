@@ -80,6 +80,11 @@ void   oracle_philox(const unsigned* ctr4, const unsigned* key2, unsigned* out4)
 void oracle_scan_sincosf(float lo, float hi, int nthreads,
                          unsigned long long* n_total, unsigned long long* n_sin_diff,
                          unsigned long long* n_cos_diff);
+/* Strided scan of the floats in [lo, hi]: counts where pm_sinf/pm_cosf
+ * differ from the correctly rounded float sin/cos (via sinl/cosl). */
+void oracle_scan_sincosf_cr(float lo, float hi, long long step, int nthreads,
+                            unsigned long long* n_total, unsigned long long* n_sin_diff,
+                            unsigned long long* n_cos_diff);
 /* acos over the 2^31 grid inputs 2*(k/2^31)-1, k = k0..k1-1 (step): counts
  * results differing from libm acos, and those whose float rounding differs. */
 void oracle_scan_acos(long long k0, long long k1, long long step, int nthreads,

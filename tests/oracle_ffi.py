@@ -77,6 +77,7 @@ def oracle():
         lib.oracle_philox.argtypes = [P(C.c_uint), P(C.c_uint), P(C.c_uint)]
         ull = P(C.c_ulonglong)
         lib.oracle_scan_sincosf.argtypes = [C.c_float, C.c_float, C.c_int, ull, ull, ull]
+        lib.oracle_scan_sincosf_cr.argtypes = [C.c_float, C.c_float, C.c_longlong, C.c_int, ull, ull, ull]
         lib.oracle_scan_acos.argtypes = [C.c_longlong, C.c_longlong, C.c_longlong, C.c_int, ull, ull, ull]
         _oracle = lib
     return _oracle

@@ -1,8 +1,8 @@
 // rt_device_math.h — device primitives of the RT_RNG_PHILOX stream spec:
 // the Philox4x32-10 stream and the portable transcendentals (DESIGN.md
-// "Portable math").  Built only from IEEE-754 +,-,*,/,sqrt, rint and bit
-// casts, compiled with -ffp-contract=off, so results are bit-identical to the
-// CPU restatement in oracle/pm_math.h.
+// "Portable math").  Built only from IEEE-754 +,-,*,/,sqrt, explicit fma,
+// rint and bit casts, compiled with -ffp-contract=off, so results are
+// bit-identical to the CPU restatement in oracle/pm_math.h.
 //
 // Register pressure: the ~60 FP64 coefficients live in a __constant__ table
 // read through the scalar unit (s_load) at the point of use; the table index
@@ -26,10 +26,10 @@ __device__ __forceinline__ int opq0()
 }
 
 enum : int {
-    // sin/cos (Taylor to degree 17 / 16 on |r| <= pi/4)
-    KC_TWO_OVER_PI = 0, KC_PIO2_1, KC_PIO2_2, KC_PIO2_3,
-    KC_S1, KC_S2, KC_S3, KC_S4, KC_S5, KC_S6, KC_S7, KC_S8,
-    KC_C1, KC_C2, KC_C3, KC_C4, KC_C5, KC_C6, KC_C7, KC_C8,
+    // sin/cos (fdlibm minimax kernels, degree 13 / 14 on |r| <= pi/4)
+    KC_TWO_OVER_PI = 0, KC_PIO2_1, KC_PIO2_1T,
+    KC_S1, KC_S2, KC_S3, KC_S4, KC_S5, KC_S6,
+    KC_C1, KC_C2, KC_C3, KC_C4, KC_C5, KC_C6,
     // acos (fdlibm)
     KC_PIO2_HI, KC_PIO2_LO, KC_PI,
     KC_PS0, KC_PS1, KC_PS2, KC_PS3, KC_PS4, KC_PS5, KC_QS1, KC_QS2, KC_QS3, KC_QS4,
@@ -41,11 +41,11 @@ enum : int {
 };
 
 __constant__ const double kC[KC_COUNT] = {
-    0x1.45f306dc9c883p-1, 0x1.921fb54400000p+0, 0x1.0b4611a600000p-34, 0x1.3198a2e000000p-69,
-    -0x1.5555555555555p-3, 0x1.1111111111111p-7, -0x1.a01a01a01a01ap-13, 0x1.71de3a556c734p-19,
-    -0x1.ae64567f544e4p-26, 0x1.6124613a86d09p-33, -0x1.ae7f3e733b81fp-41, 0x1.952c77030ad4ap-49,
-    -0x1.0000000000000p-1, 0x1.5555555555555p-5, -0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-16,
-    -0x1.27e4fb7789f5cp-22, 0x1.1eed8eff8d898p-29, -0x1.93974a8c07c9dp-37, 0x1.ae7f3e733b81fp-45,
+    0x1.45f306dc9c883p-1, 0x1.921fb54400000p+0, 0x1.0b4611a626331p-34,
+    -0x1.5555555555549p-3, 0x1.111111110f8a6p-7, -0x1.a01a019c161d5p-13, 0x1.71de357b1fe7dp-19,
+    -0x1.ae5e68a2b9cebp-26, 0x1.5d93a5acfd57cp-33,
+    0x1.555555555554cp-5, -0x1.6c16c16c15177p-10, 0x1.a01a019cb1590p-16, -0x1.27e4f809c52adp-22,
+    0x1.1ee9ebdb4b1c4p-29, -0x1.8fae9be8838d4p-37,
     0x1.921fb54442d18p+0, 0x1.1a62633145c07p-54, 0x1.921fb54442d18p+1,
     0x1.5555555555555p-3, -0x1.4d61203eb6f7dp-2, 0x1.9c1550e884455p-3, -0x1.48228b5688f3bp-5,
     0x1.9efe07501b288p-11, 0x1.23de10dfdf709p-15, -0x1.33a271c8a2d4bp+1, 0x1.02ae59c598ac8p+1,
@@ -112,14 +112,14 @@ __device__ __forceinline__ int pm_sincos(float x, double& s, double& c)
     const int b = opq0();
     const double xd = (double)x;
     const double kd = rint(xd * KCV(b, KC_TWO_OVER_PI));
-    const double r = ((xd - kd * KCV(b, KC_PIO2_1)) - kd * KCV(b, KC_PIO2_2)) - kd * KCV(b, KC_PIO2_3);
+    const double r = fma(-kd, KCV(b, KC_PIO2_1T), fma(-kd, KCV(b, KC_PIO2_1), xd));
     const double z = r * r;
-    const double ps = KCV(b, KC_S1) + z * (KCV(b, KC_S2) + z * (KCV(b, KC_S3) + z * (KCV(b, KC_S4) +
-                      z * (KCV(b, KC_S5) + z * (KCV(b, KC_S6) + z * (KCV(b, KC_S7) + z * KCV(b, KC_S8)))))));
-    const double pc = KCV(b, KC_C1) + z * (KCV(b, KC_C2) + z * (KCV(b, KC_C3) + z * (KCV(b, KC_C4) +
-                      z * (KCV(b, KC_C5) + z * (KCV(b, KC_C6) + z * (KCV(b, KC_C7) + z * KCV(b, KC_C8)))))));
-    s = r + (r * z) * ps;
-    c = 1.0 + z * pc;
+    const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, KCV(b, KC_S6), KCV(b, KC_S5)), KCV(b, KC_S4)),
+                                        KCV(b, KC_S3)), KCV(b, KC_S2)), KCV(b, KC_S1));
+    const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, KCV(b, KC_C6), KCV(b, KC_C5)), KCV(b, KC_C4)),
+                                        KCV(b, KC_C3)), KCV(b, KC_C2)), KCV(b, KC_C1));
+    s = fma(r * z, ps, r);
+    c = fma(z * z, pc, fma(-0.5, z, 1.0));
     return (int)((long long)kd & 3);
 }
 
@@ -136,9 +136,9 @@ __device__ __forceinline__ void pm_sincosf(float x, float& sn, float& cs)
 // ---- acos (fdlibm scheme) --------------------------------------------------
 __device__ __forceinline__ double pm_acos_R(int b, double z)
 {
-    const double p = z * (KCV(b, KC_PS0) + z * (KCV(b, KC_PS1) + z * (KCV(b, KC_PS2) +
-                     z * (KCV(b, KC_PS3) + z * (KCV(b, KC_PS4) + z * KCV(b, KC_PS5))))));
-    const double q = 1.0 + z * (KCV(b, KC_QS1) + z * (KCV(b, KC_QS2) + z * (KCV(b, KC_QS3) + z * KCV(b, KC_QS4))));
+    const double p = z * fma(z, fma(z, fma(z, fma(z, fma(z, KCV(b, KC_PS5), KCV(b, KC_PS4)), KCV(b, KC_PS3)),
+                                          KCV(b, KC_PS2)), KCV(b, KC_PS1)), KCV(b, KC_PS0));
+    const double q = fma(z, fma(z, fma(z, fma(z, KCV(b, KC_QS4), KCV(b, KC_QS3)), KCV(b, KC_QS2)), KCV(b, KC_QS1)), 1.0);
     return p / q;
 }
 
@@ -160,12 +160,12 @@ __device__ __forceinline__ double pm_acos(double x)
     const double s = sqrt(z);
     // x >= 0.5
     const double df = __longlong_as_double((long long)((unsigned long long)__double_as_longlong(s) & 0xffffffff00000000ull));
-    const double c = (z - df * df) / (s + df);
-    const double res_pos = 2.0 * (df + (r * s + c));
+    const double c = fma(-df, df, z) / (s + df);
+    const double res_pos = 2.0 * (df + fma(r, s, c));
     // x <= -0.5
-    const double res_neg = PI - 2.0 * (s + (r * s - PIO2_LO));
+    const double res_neg = PI - 2.0 * (s + fma(r, s, -PIO2_LO));
     // |x| < 0.5
-    const double res_small = (ix <= 0x3c600000u) ? PIO2_HI + PIO2_LO : PIO2_HI - (x - (PIO2_LO - x * r));
+    const double res_small = (ix <= 0x3c600000u) ? PIO2_HI + PIO2_LO : PIO2_HI - (x - fma(-x, r, PIO2_LO));
     double res = small ? res_small : (neg ? res_neg : res_pos);
     if (ix >= 0x3ff00000u) {                       // |x| >= 1 or NaN (x == -1 only, in the sampler)
         if (((ix - 0x3ff00000u) | (uint32_t)u) == 0u) res = neg ? PI + 2.0 * PIO2_LO : 0.0;

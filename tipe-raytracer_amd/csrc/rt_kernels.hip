@@ -66,33 +66,50 @@ __device__ __forceinline__ V3 cross(V3 u, V3 v)
     return v3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
 }
 
-// normalize(a) = a / sqrt(dot(a, a)), vec3.h:137-139, bit-exact.  The fast
-// branch runs the compiler's own gfx950 lowerings of the IEEE f64 sqrt
-// (v_rsq + Goldschmidt/Newton, 10 ops) and division (v_div_scale, v_rcp, two
-// Newton steps, mul, fma, v_div_fmas, v_div_fixup) without their range
-// scaling and special-value fixups, and shares the refined reciprocal of the
-// length among the three quotients (it depends only on the divisor).  Those
-// fixups are identities when dot(a,a) is in [2^-760, 2^760] and no component
-// is below 2^-900 in magnitude (no scaling, no zero/inf/denormal operand or
-// intermediate); other lanes -- zero components, NaN, extreme lengths -- take
-// the generic `/` and `sqrt`.  rt_selftest_math op 8 checks the two agree.
+// Exact f64 sqrt and division without their range fixups.  These are the
+// compiler's own gfx950 lowerings of the IEEE operations -- sqrt: v_rsq +
+// Goldschmidt/Newton (10 ops); x/d: v_div_scale, v_rcp, two Newton steps on
+// the reciprocal, mul, fma, v_div_fmas, v_div_fixup -- with the scaling and
+// special-value steps dropped.  Those steps are identities under the guards
+// each call site checks (no zero/inf/NaN/denormal operand or intermediate,
+// operand exponents well inside the range), so the results are bit-identical
+// to `sqrt` and `/`; lanes outside the guards take the generic operations.
+// The refined reciprocal depends only on the divisor, so one rcp_refined
+// serves every quotient by the same d.  rt_selftest_math op 8 and the parity
+// suite check them.
+__device__ __forceinline__ double sqrt_core(double x)          // x in [2^-760, 2^760]
+{
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    g = fma(fma(-g, g, x), h, g);
+    return fma(fma(-g, g, x), h, g);
+}
+__device__ __forceinline__ double rcp_refined(double d)         // d in [2^-400, 2^400]
+{
+    double rc = __builtin_amdgcn_rcp(d);
+    rc = fma(rc, fma(-d, rc, 1.0), rc);
+    return fma(rc, fma(-d, rc, 1.0), rc);
+}
+__device__ __forceinline__ double div_core(double x, double d, double rc)   // |x| in [2^-900, 2^900]
+{
+    const double q = x * rc;
+    return fma(fma(-d, q, x), rc, q);
+}
+
+// normalize(a) = a / sqrt(dot(a, a)), vec3.h:137-139, bit-exact: fast lanes
+// need dot(a,a) in [2^-760, 2^760] and every |component| >= 2^-900 (so zero
+// components, NaN and extreme lengths take the generic path).
 __device__ __forceinline__ V3 normalize(V3 a)
 {
     const double n2 = dot(a, a);
     const double mn = fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
     if (n2 >= 0x1p-760 && n2 <= 0x1p760 && mn >= 0x1p-900) {
-        const double y = __builtin_amdgcn_rsq(n2);
-        double g = n2 * y, h = y * 0.5;
-        const double r = fma(-h, g, 0.5);
-        g = fma(g, r, g);
-        h = fma(h, r, h);
-        g = fma(fma(-g, g, n2), h, g);
-        const double L = fma(fma(-g, g, n2), h, g);           // == sqrt(n2)
-        double rc = __builtin_amdgcn_rcp(L);
-        rc = fma(rc, fma(-L, rc, 1.0), rc);
-        rc = fma(rc, fma(-L, rc, 1.0), rc);
-        const double qx = a.x * rc, qy = a.y * rc, qz = a.z * rc;
-        return v3(fma(fma(-L, qx, a.x), rc, qx), fma(fma(-L, qy, a.y), rc, qy), fma(fma(-L, qz, a.z), rc, qz));
+        const double L = sqrt_core(n2);
+        const double rc = rcp_refined(L);
+        return v3(div_core(a.x, L, rc), div_core(a.y, L, rc), div_core(a.z, L, rc));
     }
     return divs(a, sqrt(n2));
 }
@@ -130,23 +147,33 @@ __device__ __forceinline__ double dinf() { return __longlong_as_double(0x7ff0000
 // hit_sphere, sphere.h:13-47, exact reference arithmetic.  two_a = 2*a and
 // four_a = 4*a with a = dot(d, d) (`4*a*c` == (4*a)*c).  A negative
 // numerator decides t < 1e-4 without the division (2a > 0).
+//
+// With fast (two_a in [2^-100, 2^100], rc2a = rcp_refined(two_a)) the
+// divisions run div_core: a hit needs n >= 1e-4*two_a >> 2^-900, and
+// disc <= 2^760 bounds |n| by 2^512, so every quotient that can decide or
+// become t is exact; smaller n give t < 1e-4 on both paths.
 __device__ __forceinline__ bool sphere_exact(double cx, double cy, double cz, double r2, const V3 o, const V3 d,
-                                             double two_a, double four_a, double& t)
+                                             double two_a, double four_a, bool fast, double rc2a, double& t)
 {
     const double ocx = o.x - cx, ocy = o.y - cy, ocz = o.z - cz;
     const double b = 2.0 * (ocx * d.x + ocy * d.y + ocz * d.z);
     const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
     const double disc = b * b - four_a * c;
     if (!(disc > 0)) return false;
-    const double sq = sqrt(disc);
+    const bool f = fast && disc >= 0x1p-760 && disc <= 0x1p760;
+    double sq;
+    if (f) sq = sqrt_core(disc);
+    else sq = sqrt(disc);
     const double n1 = -b - sq;
     if (!(n1 < 0.0)) {
-        t = n1 / two_a;
+        if (f) t = div_core(n1, two_a, rc2a);
+        else t = n1 / two_a;
         if (t >= 0.0001) return true;
     }
     const double n2 = -b + sq;
     if (!(n2 < 0.0)) {
-        t = n2 / two_a;
+        if (f) t = div_core(n2, two_a, rc2a);
+        else t = n2 / two_a;
         if (t >= 0.0001) return true;
     }
     return false;
@@ -163,7 +190,8 @@ __device__ __forceinline__ bool sphere_exact(double cx, double cy, double cz, do
 // interval end points.
 template <bool COUNT>
 __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, const V3 d, double two_a,
-                                               double four_a, double inv2a, double& t_best, Cnt& cnt)
+                                               double four_a, double inv2a, bool fast, double rc2a,
+                                               double& t_best, Cnt& cnt)
 {
     const cdptr sg = (cdptr)kp.sph;
     const double INF = dinf();
@@ -227,7 +255,7 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     int win = -1;
     if (!amb && bk >= 0) {
         const SphGeo s = kp.sph[bk];
-        if (sphere_exact(s.cx, s.cy, s.cz, s.r2, o, d, two_a, four_a, t)) win = bk;
+        if (sphere_exact(s.cx, s.cy, s.cz, s.r2, o, d, two_a, four_a, fast, rc2a, t)) win = bk;
         else amb = true;     // cannot happen within the bound; stay exact anyway
     }
     if (amb) {               // exact reference scan for this ray
@@ -236,7 +264,8 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
         win = -1;
         for (int k = 0; k < kp.ns_pad; ++k) {
             double tk;
-            if (sphere_exact(sg[4 * k], sg[4 * k + 1], sg[4 * k + 2], sg[4 * k + 3], o, d, two_a, four_a, tk) &&
+            if (sphere_exact(sg[4 * k], sg[4 * k + 1], sg[4 * k + 2], sg[4 * k + 3], o, d, two_a, four_a, fast, rc2a,
+                             tk) &&
                 tk < t) {
                 t = tk;
                 win = k;
@@ -256,14 +285,18 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
     const double a = dot(d, d);          // sphere.h:20 (same for every sphere)
     const double two_a = 2 * a;          // sphere.h:27,36
     const double four_a = 4 * a;         // sphere.h:24
-    const double inv2a = 1.0 / two_a;    // candidate pass only
+    const bool fast = two_a >= 0x1p-100 && two_a <= 0x1p100;
+    const double rc2a = rcp_refined(two_a);
+    double inv2a;                        // RN(1 / two_a), candidate pass only
+    if (fast) inv2a = div_core(1.0, two_a, rc2a);
+    else inv2a = 1.0 / two_a;
     if (COUNT) {
         cnt.c[RT_CNT_CASTS] += 1;
         cnt.c[RT_CNT_SPHERE_TESTS] += (unsigned long long)kp.ns;
         cnt.c[RT_CNT_TRI_TESTS] += (unsigned long long)kp.nt;
     }
     double best;
-    int win = spheres_closest<COUNT>(kp, o, d, two_a, four_a, inv2a, best, cnt);
+    int win = spheres_closest<COUNT>(kp, o, d, two_a, four_a, inv2a, fast, rc2a, best, cnt);
     int kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
     const TriGeo* __restrict__ tri = kp.tri;
     for (int k = 0; k < kp.nt; ++k) {                     // hit_triangle, mesh.h:70-94
@@ -272,7 +305,9 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
         if (det >= 1E-6) {
             const V3 ao = v3(o.x - g.ax, o.y - g.ay, o.z - g.az);
             const V3 dao = cross(ao, d);
-            const double invDet = 1 / det;
+            double invDet;
+            if (det <= 0x1p400) invDet = div_core(1.0, det, rcp_refined(det));   // det >= 1e-6: exact
+            else invDet = 1 / det;
             const double dst = (ao.x * g.nx + ao.y * g.ny + ao.z * g.nz) * invDet;
             if (dst >= 0.0000001 && dst < best) {
                 const double u = (g.acx * dao.x + g.acy * dao.y + g.acz * dao.z) * invDet;
