@@ -76,10 +76,19 @@ typedef struct rt_params {
                                           GPU count) that lets one pixel's
                                           samples run on P wavefronts          */
     unsigned long long seed;           /* Philox key                             */
+    int accel;                         /* RT_ACCEL_*: triangle traversal          */
 } rt_params;
 
+/* rt_params.accel.  AUTO: scenes with more than 32 triangles get a BVH at
+ * rt_scene_upload and closest-hit traverses it (the hit chosen is still the
+ * reference's: the lexicographic minimum of (dst, triangle index) over the
+ * same exact tests, DESIGN.md "BVH"); NONE: test every triangle, as
+ * main.c:80-90. */
+#define RT_ACCEL_AUTO 0
+#define RT_ACCEL_NONE 1
+
 /* Fills defaults: RT_RNG_PHILOX, seed 1010 (main_cuda.cu's curand seed),
- * compat_int_truncation 1, spp_chunks 1, everything else zero. */
+ * compat_int_truncation 1, spp_chunks 1, RT_ACCEL_AUTO, everything else zero. */
 void rt_params_init(rt_params* p);
 
 /* ---- lifecycle ---------------------------------------------------------- */
@@ -161,6 +170,10 @@ enum {
     RT_CNT_RNG_DRAWS,     /* 31-bit draws consumed                         */
     RT_CNT_EXACT_RESCANS, /* sphere scans redone exactly (candidate pass
                              ambiguous; GPU diagnostic, the oracle reports 0) */
+    RT_CNT_BVH_NODES,     /* BVH nodes visited (GPU diagnostic)            */
+    RT_CNT_BVH_TRI_TESTS, /* triangles actually tested through the BVH
+                             (GPU diagnostic; RT_CNT_TRI_TESTS keeps the
+                             reference's brute-force count)              */
     RT_NCOUNTERS
 };
 /* Same traversal as rt_render_async, no frame; adds event counts into the

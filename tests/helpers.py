@@ -33,22 +33,21 @@ def cornell(extra=()):
     return SceneBundle(scenes.cornell_spheres(extra=extra))
 
 
-def pyramid_scene(move=(-0.6, -1.0, -2.0)):
-    tris, qm, mats, tw, th, nm = scenes.load_mesh_fixture("pyramide")
-    for t in tris:
-        for P in (t.A, t.B, t.C):
-            P.e[0] += move[0]
-            P.e[1] += move[1]
-            P.e[2] += move[2]
-    return SceneBundle(scenes.cornell_spheres(), (tris, qm, mats, tw, th, nm))
+def pyramid_scene(move=scenes.PYRAMID_MOVE):
+    return SceneBundle(scenes.cornell_spheres(), scenes.moved(scenes.load_mesh_fixture("pyramide"), move))
+
+
+def tree_scene(move=scenes.TREE_MOVE):
+    """C4: README spheres + 1tree_tri.obj (1320 tris, Kd-flat materials)."""
+    return SceneBundle(scenes.cornell_spheres(), scenes.moved(scenes.load_tree_fixture(), move))
 
 
 def params(W, H, spp, bounces, use_ao=False, ao=2.5, rng=RT_RNG_PHILOX, seed=1010, compat=1, cam=None,
-           aperture=(0.0, 0.0), focus=3.0, chunks=1):
+           aperture=(0.0, 0.0), focus=3.0, chunks=1, accel=0):
     if cam is None:
         cam = readme_camera_oracle()
     return tipe_rt.make_params(W, H, spp, bounces, cam, focus=focus, aperture=aperture, use_ao=use_ao, ao=ao,
-                               seed=seed, rng=rng, compat=compat, chunks=chunks)
+                               seed=seed, rng=rng, compat=compat, chunks=chunks, accel=accel)
 
 
 def oracle_render(bundle, p, row_hi=None, row_lo=0, nthreads=1, counters=False):

@@ -174,6 +174,54 @@ def test_mineways_alpha_holes():
     check_parity(bundle, helpers.params(40, 30, 4, 6))
 
 
+def test_tree_ao_c4_scene():
+    """C4 scene: README spheres + 1tree_tri.obj (1320 tris,
+    Kd-flat materials, leaves = material 1 -> emitter override), AO on with
+    the int-truncated intensity, 8 bounces."""
+    ref = check_parity(helpers.tree_scene(), helpers.params(32, 24, 4, 8, use_ao=True))
+    assert ref["canva"].max() > 0
+
+
+def test_tree_brute_force_path_matches():
+    """Same C4 scene through the every-triangle scan (RT_ACCEL_NONE): the
+    triangle arrays stay in BVH leaf order, so this also checks the
+    (dst, caller index) tie-break of the unordered scan."""
+    check_parity(helpers.tree_scene(), helpers.params(24, 18, 3, 8, use_ao=True, accel=1))
+
+
+def duplicate_mesh_scene(n=150, seed=5):
+    """Random triangles, each present twice (second copy later in the list)
+    with a different flat material: every hit on a pair is an exact dst tie
+    the reference resolves to the first copy (strict < in list order)."""
+    from tipe_rt.types import Triangle, Material, Vec3
+    rng = np.random.default_rng(seed)
+    base = []
+    for _ in range(n):
+        c = rng.uniform([-1.5, -1.5, -3.6], [1.5, 1.5, -1.0])
+        e = rng.normal(size=(2, 3)) * 0.35
+        base.append((c, c + e[0], c + e[1]))
+    order = rng.permutation(2 * n)               # caller list: copies interleaved in random order
+    tris = (Triangle * (2 * n))()
+    qm = (C.c_int * (2 * n))()
+    first_seen = set()
+    for slot, k in enumerate(order):
+        A, B, Cc = base[k % n]
+        tris[slot].A, tris[slot].B, tris[slot].C = Vec3(*A), Vec3(*B), Vec3(*Cc)
+        qm[slot] = 0 if (k % n) not in first_seen else 2
+        first_seen.add(k % n)
+    mats = (Material * 3)()
+    cols = [(0.9, 0.2, 0.1), (0.5, 0.5, 0.5), (0.1, 0.3, 0.9)]
+    for m in range(3):
+        mats[m] = tipe_rt.scenes.material(cols[m], (0, 0, 0), 0.0, 0.0, 1.0, 0.0)
+    return helpers.SceneBundle(tipe_rt.scenes.cornell_spheres(), (tris, qm, mats, 1, 1, 3))
+
+
+def test_bvh_tie_break_on_duplicate_triangles():
+    bundle = duplicate_mesh_scene()
+    check_parity(bundle, helpers.params(40, 30, 4, 6))
+    check_parity(bundle, helpers.params(24, 18, 2, 6, accel=1))
+
+
 def test_counters_match_oracle():
     import torch
     bundle = helpers.pyramid_scene()

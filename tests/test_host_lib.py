@@ -20,37 +20,7 @@ REF = "/root/reference/model3D"
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-class Mesh(C.Structure):
-    _fields_ = [("triangles", C.POINTER(Triangle)), ("nbTriangles", C.c_int),
-                ("quelMatPourTri", C.POINTER(C.c_int)), ("nbMaterials", C.c_int),
-                ("material_names", C.POINTER(C.c_char_p)), ("texture_paths", C.POINTER(C.c_char_p)),
-                ("kd", C.POINTER(Vec3)), ("ns", C.POINTER(C.c_double))]
-
-
-def host():
-    H = tipe_rt.host()
-    H.rt_host_load_obj.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.POINTER(Mesh)]
-    H.rt_host_load_textures.argtypes = [C.POINTER(Mesh), C.c_int, C.POINTER(C.POINTER(Material)),
-                                        C.POINTER(C.c_int), C.POINTER(C.c_int)]
-    H.rt_host_free_mesh.argtypes = [C.POINTER(Mesh)]
-    H.rt_host_read_ppm.argtypes = [C.c_char_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
-                                   C.POINTER(C.POINTER(C.c_int))]
-    H.rt_host_write_ppm.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int]
-    H.rt_host_free.argtypes = [C.c_void_p]
-    H.rt_host_move_mesh.argtypes = [C.c_double, C.c_double, C.c_double, C.POINTER(Triangle), C.c_int]
-    return H
-
-
-def load(obj, mtl, mode=0, kd_fallback=1):
-    H = host()
-    m = Mesh()
-    rc = H.rt_host_load_obj(obj.encode(), mtl.encode() if mtl else None, mode, C.byref(m))
-    if rc:
-        return rc, None, None
-    mats = C.POINTER(Material)()
-    tw, th = C.c_int(), C.c_int()
-    rc = H.rt_host_load_textures(C.byref(m), kd_fallback, C.byref(mats), C.byref(tw), C.byref(th))
-    return rc, m, (mats, tw.value, th.value)
+from tipe_rt.host_io import Mesh, lib as host, load  # noqa: E402  (the ctypes mirror under test)
 
 
 def test_init_camera_matches_survey_kat():

@@ -16,6 +16,7 @@
 
 #include "rt/rt.h"
 #include "rt_internal.h"
+#include "rt_bvh.h"
 
 using namespace rt;
 
@@ -91,6 +92,7 @@ int validate_params(const rt_params* p)
                     "RT_RNG_GLIBC is one sequential rand() stream with data-dependent draw counts; "
                     "only the CPU oracle replays it");
     if (p->rng != RT_RNG_PHILOX) return fail(RT_EINVAL, "unknown rng %d", p->rng);
+    if (p->accel != RT_ACCEL_AUTO && p->accel != RT_ACCEL_NONE) return fail(RT_EINVAL, "unknown accel %d", p->accel);
     if ((unsigned long long)p->largeur_image * (unsigned long long)p->hauteur_image > 0xffffffffull)
         return fail(RT_EUNSUPPORTED, "pixel index exceeds the 32-bit Philox counter word");
     return RT_OK;
@@ -117,6 +119,10 @@ struct rt_device_scene {
     TriGeo* tri = nullptr;
     TriTex* tri_tex = nullptr;
     DevMat* texels = nullptr;
+    BvhNode* bvh = nullptr;          // null: no BVH (few triangles)
+    int* tri_orig = nullptr;         // leaf order -> caller's triangle index
+    int bvh_nodes = 0, bvh_depth = 0;
+    double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0;
 };
 
 namespace {
@@ -137,6 +143,8 @@ void free_scene(rt_device_scene* s)
     (void)hipFree(s->tri);
     (void)hipFree(s->tri_tex);
     (void)hipFree(s->texels);
+    (void)hipFree(s->bvh);
+    (void)hipFree(s->tri_orig);
     delete s;
 }
 
@@ -168,6 +176,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.tri = sc->tri;
     kp.tri_tex = sc->tri_tex;
     kp.texels = sc->texels;
+    kp.tri_orig = sc->tri_orig;
     kp.ns = sc->ns;
     kp.ns_pad = sc->ns_pad;
     kp.nt = sc->nt;
@@ -208,6 +217,16 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.n_tiles = t->n_tiles;
     kp.row_end = p->hauteur_image;
     kp.local_rows = t->n_tiles * t->tile_rows;
+    // The BVH padding assumed every ray origin within r_scene (rt_bvh.cpp);
+    // primary rays start at the camera origin + (dx, dy, 0), |dx| <= |ox|/2.
+    double cam = 0.0;
+    for (int i = 0; i < 3; ++i) cam = std::max(cam, std::fabs(p->cam.origin.e[i]));
+    cam += 0.5 * (std::fabs(ox) + std::fabs(oy));
+    if (sc->bvh && p->accel == RT_ACCEL_AUTO && cam <= sc->r_scene) {
+        kp.bvh = sc->bvh;
+        kp.bvh_srel = sc->s_rel;
+        kp.bvh_sabs = sc->s_abs;
+    }
     return RT_OK;
 }
 
@@ -355,6 +374,32 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         x.mat = scene->quelMatPourTri[i];
         x.pad = 0;
     }
+    // Triangle BVH (rt_bvh.cpp) over scenes with more than 32 triangles; the
+    // triangle arrays are then stored in leaf order.  r_scene bounds every
+    // coordinate a ray origin can take on the scene's surfaces.
+    BvhBuild bvh;
+    if (scene->nbTriangles > 32) {
+        double r = 1.0;
+        for (int i = 0; i < scene->nbSpheres; ++i) {
+            const rt_sphere& q = scene->sphere_list[i];
+            for (int a = 0; a < 3; ++a) r = std::max(r, std::fabs(q.center.e[a]) + std::fabs(q.radius));
+        }
+        for (int i = 0; i < scene->nbTriangles; ++i) {
+            const rt_triangle& t = scene->triangle_list[i];
+            for (int a = 0; a < 3; ++a)
+                r = std::max({r, std::fabs(t.A.e[a]), std::fabs(t.B.e[a]), std::fabs(t.C.e[a])});
+        }
+        if (std::isfinite(r) && build_bvh(tri.data(), scene->nbTriangles, r, bvh)) {
+            std::vector<TriGeo> tri2(tri.size());
+            std::vector<TriTex> tex2(tex.size());
+            for (size_t k = 0; k < tri.size(); ++k) {
+                tri2[k] = tri[(size_t)bvh.order[k]];
+                tex2[k] = tex[(size_t)bvh.order[k]];
+            }
+            tri.swap(tri2);
+            tex.swap(tex2);
+        }
+    }
     std::vector<DevMat> texels;
     long long n_texels = 0;
     if (scene->nbTriangles > 0) {
@@ -371,8 +416,14 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->tw = scene->nbTriangles > 0 ? scene->tex_width : 1;
     ds->th = scene->nbTriangles > 0 ? scene->tex_height : 1;
     ds->n_texels = n_texels;
+    ds->bvh_nodes = (int)bvh.nodes.size();
+    ds->bvh_depth = bvh.depth;
+    ds->s_rel = bvh.s_rel;
+    ds->s_abs = bvh.s_abs;
+    ds->r_scene = bvh.r_scene;
     if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
-        (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels))) {
+        (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels)) ||
+        (rc = upload(&ds->bvh, bvh.nodes)) || (rc = upload(&ds->tri_orig, bvh.order))) {
         free_scene(ds);
         return rc;
     }

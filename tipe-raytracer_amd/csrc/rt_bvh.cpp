@@ -1,0 +1,222 @@
+// rt_bvh.cpp — host build of the triangle BVH used by the render kernel
+// (the reference scans every triangle, main.c:80-90, and
+// its CUDA path only has a per-mesh slab box, triangle.hu:42-59).
+//
+// Binary BVH, binned SAH (16 bins on the widest centroid axis), leaves of at
+// most 4 triangles (more only at the depth cap).  Each node stores the boxes
+// of BOTH children, so one 128-byte node fetch decides both descents.  Node 0
+// is the root split; triangles are reordered into leaf order and the kernel
+// keeps each one's original index for the reference's tie-break.
+//
+// Exactness: the BVH only decides which triangles are *tested*; every test
+// is the reference arithmetic and the winner is the lexicographic minimum of
+// (dst, original index) -- what the reference's in-order strict-< scan
+// returns.  So culling must never drop a triangle that could win or tie.
+// The boxes are padded, and the kernel's distance cull carries a slack, by
+// rigorous bounds on the rounding error of the reference test (DESIGN.md
+// "BVH"): with det >= 1e-6 (mesh.h:79) the computed barycentrics of an
+// accepted hit are within eps_k of exact ones, so the ray meets triangle k's
+// plane inside k's box grown by
+//     delta_k = (e1+e2) * (2^-44 * 1e6 * ((e1+e2)*4R + 6*e1*e2) + 2^-48)
+// (e1, e2 = |B-A|, |C-A|; R bounds every coordinate and ray origin), and the
+// computed dst is within  2^-44 * 1e6 * maxN * (t + R)  of that plane hit
+// (maxN = max |N|).  The constants carry a factor >= 8 over the
+// first-order bounds (3-term dot/cross products, one division).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "rt_bvh.h"
+
+namespace rt {
+namespace {
+
+struct Box {
+    double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL};
+    double hi[3] = {-HUGE_VAL, -HUGE_VAL, -HUGE_VAL};
+    void grow(const Box& b)
+    {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], b.lo[a]);
+            hi[a] = std::max(hi[a], b.hi[a]);
+        }
+    }
+    void grow(const double* p)
+    {
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], p[a]);
+            hi[a] = std::max(hi[a], p[a]);
+        }
+    }
+    double area() const
+    {
+        if (lo[0] > hi[0]) return 0.0;
+        const double x = hi[0] - lo[0], y = hi[1] - lo[1], z = hi[2] - lo[2];
+        return 2.0 * (x * y + y * z + z * x);
+    }
+};
+
+struct Prim {
+    Box box;
+    double c[3];
+    int idx;
+};
+
+struct Ref {
+    bool leaf;
+    int index;   // node index, or first prim of the leaf
+    int count;
+    Box box;
+};
+
+constexpr int kLeaf = 4;
+constexpr int kBins = 16;
+
+struct Builder {
+    std::vector<Prim>& P;
+    std::vector<BvhNode>& nodes;
+    int max_depth = 0;
+
+    Ref leaf(int b, int e, const Box& box) { return Ref{true, b, e - b, box}; }
+
+    // SAH split position in [b, e) after partitioning, or -1.
+    int split(int b, int e, const Box& cbox, int depth)
+    {
+        const int n = e - b;
+        int axis = 0;
+        double ext = -1.0;
+        for (int a = 0; a < 3; ++a)
+            if (cbox.hi[a] - cbox.lo[a] > ext) {
+                ext = cbox.hi[a] - cbox.lo[a];
+                axis = a;
+            }
+        int mid = -1;
+        if (ext > 0.0) {
+            Box bb[kBins];
+            int bc[kBins] = {0};
+            const double scale = kBins / ext;
+            auto bin_of = [&](const Prim& p) {
+                int k = (int)((p.c[axis] - cbox.lo[axis]) * scale);
+                return k < 0 ? 0 : (k >= kBins ? kBins - 1 : k);
+            };
+            for (int i = b; i < e; ++i) {
+                const int k = bin_of(P[(size_t)i]);
+                bb[k].grow(P[(size_t)i].box);
+                ++bc[k];
+            }
+            double best = HUGE_VAL;
+            int best_k = -1;
+            Box left;
+            int nl = 0;
+            for (int k = 0; k < kBins - 1; ++k) {
+                left.grow(bb[k]);
+                nl += bc[k];
+                Box right;
+                int nr = 0;
+                for (int j = k + 1; j < kBins; ++j) {
+                    right.grow(bb[j]);
+                    nr += bc[j];
+                }
+                if (nl == 0 || nr == 0) continue;
+                const double cost = left.area() * nl + right.area() * nr;
+                if (cost < best) {
+                    best = cost;
+                    best_k = k;
+                }
+            }
+            Box all;
+            for (int i = b; i < e; ++i) all.grow(P[(size_t)i].box);
+            const bool worth = best_k >= 0 && (n > 2 * kLeaf || best < all.area() * n);
+            if (worth) {
+                auto it = std::partition(P.begin() + b, P.begin() + e,
+                                         [&](const Prim& p) { return bin_of(p) <= best_k; });
+                mid = (int)(it - P.begin());
+                if (mid == b || mid == e) mid = -1;
+            }
+        }
+        if (mid < 0 && n > kLeaf && depth < kMaxDepth) {     // degenerate centroids: median on index
+            mid = b + n / 2;
+            std::nth_element(P.begin() + b, P.begin() + mid, P.begin() + e,
+                             [&](const Prim& x, const Prim& y) { return x.c[axis] < y.c[axis]; });
+        }
+        return mid;
+    }
+
+    Ref build(int b, int e, int depth)
+    {
+        Box box, cbox;
+        for (int i = b; i < e; ++i) {
+            box.grow(P[(size_t)i].box);
+            cbox.grow(P[(size_t)i].c);
+        }
+        max_depth = std::max(max_depth, depth);
+        if (e - b <= kLeaf || depth >= kMaxDepth) return leaf(b, e, box);
+        const int mid = split(b, e, cbox, depth);
+        if (mid < 0) return leaf(b, e, box);
+        const int idx = (int)nodes.size();
+        nodes.emplace_back();
+        const Ref L = build(b, mid, depth + 1);
+        const Ref R = build(mid, e, depth + 1);
+        BvhNode& nd = nodes[(size_t)idx];
+        const Ref* ch[2] = {&L, &R};
+        for (int c = 0; c < 2; ++c) {
+            for (int a = 0; a < 3; ++a) {
+                nd.lo[c][a] = ch[c]->box.lo[a];
+                nd.hi[c][a] = ch[c]->box.hi[a];
+            }
+            nd.child[c] = ch[c]->index;
+            nd.count[c] = ch[c]->leaf ? ch[c]->count : 0;
+        }
+        return Ref{false, idx, 0, box};
+    }
+};
+
+double norm3(double x, double y, double z) { return std::sqrt(x * x + y * y + z * z); }
+
+}  // namespace
+
+bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
+{
+    out = BvhBuild();
+    if (nt <= kLeaf) return false;
+    double maxN = 0.0;
+    std::vector<Prim> P((size_t)nt);
+    for (int i = 0; i < nt; ++i) {
+        const TriGeo& g = tri[i];
+        const double e1 = norm3(g.abx, g.aby, g.abz), e2 = norm3(g.acx, g.acy, g.acz);
+        maxN = std::max(maxN, norm3(g.nx, g.ny, g.nz));
+        const double delta = (e1 + e2) * (std::ldexp(1e6, -44) * ((e1 + e2) * 4.0 * r_scene + 6.0 * e1 * e2) +
+                                          std::ldexp(1.0, -48)) +
+                             std::ldexp(r_scene, -48);
+        const double A[3] = {g.ax, g.ay, g.az};
+        const double B[3] = {g.ax + g.abx, g.ay + g.aby, g.az + g.abz};
+        const double C[3] = {g.ax + g.acx, g.ay + g.acy, g.az + g.acz};
+        Prim& p = P[(size_t)i];
+        p.box.grow(A);
+        p.box.grow(B);
+        p.box.grow(C);
+        for (int a = 0; a < 3; ++a) {
+            p.box.lo[a] -= delta + std::fabs(p.box.lo[a]) * std::ldexp(1.0, -50);
+            p.box.hi[a] += delta + std::fabs(p.box.hi[a]) * std::ldexp(1.0, -50);
+            p.c[a] = 0.5 * (p.box.lo[a] + p.box.hi[a]);
+        }
+        p.idx = i;
+    }
+    Builder bld{P, out.nodes};
+    const Ref root = bld.build(0, nt, 0);
+    if (root.leaf || out.nodes.size() >= 65535) {        // uint16 traversal stack entries
+        out = BvhBuild();
+        return false;
+    }
+    out.order.resize((size_t)nt);
+    for (int i = 0; i < nt; ++i) out.order[(size_t)i] = P[(size_t)i].idx;
+    out.depth = bld.max_depth;
+    const double k = std::ldexp(1e6, -44) * maxN;
+    out.s_rel = k + std::ldexp(1.0, -48);
+    out.s_abs = k * r_scene + std::ldexp(r_scene, -48);
+    out.r_scene = r_scene;
+    return true;
+}
+
+}  // namespace rt

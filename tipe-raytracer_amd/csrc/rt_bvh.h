@@ -1,0 +1,37 @@
+// rt_bvh.h — triangle BVH layout shared by the host builder (rt_bvh.cpp), the
+// C-ABI (rt_api.cpp) and the kernel (rt_kernels.hip).
+#pragma once
+#include <vector>
+
+#include "rt_internal.h"
+
+namespace rt {
+
+constexpr int kMaxDepth = 30;       // the kernel's LDS stack holds kMaxDepth + 1 entries
+
+// One internal node: the padded boxes of both children (one 128-byte fetch
+// per visit).  count[c] > 0: child c is a leaf of count[c] triangles starting
+// at child[c] (leaf order); count[c] == 0: child[c] is a node index.
+struct BvhNode {
+    double lo[2][3];
+    double hi[2][3];
+    int child[2];
+    int count[2];
+    double pad[2];
+};
+static_assert(sizeof(BvhNode) == 128, "BvhNode");
+
+struct BvhBuild {
+    std::vector<BvhNode> nodes;     // node 0 = root split
+    std::vector<int> order;         // leaf order -> original triangle index
+    int depth = 0;
+    double s_rel = 0.0, s_abs = 0.0;   // distance-cull slack (rt_bvh.cpp header)
+    double r_scene = 0.0;              // coordinate bound the padding assumed
+};
+
+// Builds over nt precomputed triangles whose coordinates (and every ray
+// origin) are bounded by r_scene in magnitude.  false: no BVH (too few
+// triangles or too many nodes) -> brute-force scan.
+bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out);
+
+}  // namespace rt

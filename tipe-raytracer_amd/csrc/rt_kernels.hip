@@ -43,6 +43,7 @@
 
 #include "rt/rt.h"
 #include "rt_internal.h"
+#include "rt_bvh.h"
 #include "rt_device_math.h"
 
 #ifndef RT_WAVES_PER_SIMD
@@ -276,9 +277,110 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     return win;
 }
 
+// hit_triangle, mesh.h:70-94, exact reference arithmetic, folded into the
+// running closest hit.  Acceptance is the reference's `dst >= 1e-7 && dst <
+// best` plus its in-order tie-break: when the triangles are not scanned in
+// the caller's order (BVH leaf order), an equal dst replaces a triangle
+// winner with a larger caller index (orig).  det >= 1e-6 >= 2^-400 puts
+// 1/det on the exact fast division (div_core).
+template <bool COUNT>
+__device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, const V3 d, double& best, int& kind,
+                                         int& win, int& win_orig)
+{
+    const TriGeo g = kp.tri[k];
+    const double det = -(d.x * g.nx + d.y * g.ny + d.z * g.nz);
+    if (det >= 1E-6) {
+        const V3 ao = v3(o.x - g.ax, o.y - g.ay, o.z - g.az);
+        const V3 dao = cross(ao, d);
+        double invDet;
+        if (det <= 0x1p400) invDet = div_core(1.0, det, rcp_refined(det));
+        else invDet = 1 / det;
+        const double dst = (ao.x * g.nx + ao.y * g.ny + ao.z * g.nz) * invDet;
+        if (dst >= 0.0000001 && dst <= best) {
+            const int orig = kp.tri_orig ? kp.tri_orig[k] : k;
+            if (dst < best || (kind == HIT_TRI && orig < win_orig)) {
+                const double u = (g.acx * dao.x + g.acy * dao.y + g.acz * dao.z) * invDet;
+                const double v = -(g.abx * dao.x + g.aby * dao.y + g.abz * dao.z) * invDet;
+                const double w = 1 - u - v;
+                if (u >= 0.0000001 && v >= 0.0000001 && w >= 0.0000001) {
+                    best = dst;
+                    kind = HIT_TRI;
+                    win = k;
+                    win_orig = orig;
+                }
+            }
+        }
+    }
+}
+
+// Triangle BVH traversal (rt_bvh.h layout; host build rt_bvh.cpp).  One
+// 128-byte node holds both child boxes; leaf children are tested on the
+// spot, a doubly-hit pair descends into the nearer box and pushes the other
+// on a per-lane LDS stack ([depth][256] uint16, conflict-free).  A box is
+// skipped only when no triangle in it can win or tie (rt_bvh.cpp): the ray
+// misses the padded box, leaves it behind the origin (tmax < -sabs), or
+// enters it beyond best*(1+srel) + sabs.  Slab reciprocals use |d_i| >=
+// 2^-200, which keeps the products finite without changing any decision
+// for unit-length directions.
+template <bool COUNT>
+__device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3 d, double& best, int& kind,
+                                         int& win, int& win_orig, Cnt& cnt)
+{
+    __shared__ unsigned short stk_lds[(kMaxDepth + 2) * 256];
+    unsigned short* stk = stk_lds + threadIdx.x;
+    const double lim = 0x1p-200;
+    const double ix = 1.0 / (fabs(d.x) < lim ? copysign(lim, d.x) : d.x);
+    const double iy = 1.0 / (fabs(d.y) < lim ? copysign(lim, d.y) : d.y);
+    const double iz = 1.0 / (fabs(d.z) < lim ? copysign(lim, d.z) : d.z);
+    const double srel = 1.0 + kp.bvh_srel, sabs = kp.bvh_sabs;
+    int node = 0, sp = 0;
+    while (true) {
+        const BvhNode* nd = kp.bvh + node;
+        if (COUNT) cnt.c[RT_CNT_BVH_NODES] += 1;
+        bool h[2];
+        double tn[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const double x0 = (nd->lo[c][0] - o.x) * ix, x1 = (nd->hi[c][0] - o.x) * ix;
+            const double y0 = (nd->lo[c][1] - o.y) * iy, y1 = (nd->hi[c][1] - o.y) * iy;
+            const double z0 = (nd->lo[c][2] - o.z) * iz, z1 = (nd->hi[c][2] - o.z) * iz;
+            const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
+            const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
+            h[c] = tmin <= tmax && tmax >= -sabs && tmin <= best * srel + sabs;
+            tn[c] = tmin;
+        }
+        const int c0 = nd->child[0], c1 = nd->child[1];
+        const int n0 = nd->count[0], n1 = nd->count[1];
+        if (h[0] && n0 > 0) {
+            for (int k = c0; k < c0 + n0; ++k) tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
+            if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)n0;
+            h[0] = false;
+        }
+        if (h[1] && n1 > 0) {
+            for (int k = c1; k < c1 + n1; ++k) tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
+            if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)n1;
+            h[1] = false;
+        }
+        if (h[0] && h[1]) {
+            const bool far0 = tn[1] < tn[0];
+            stk[sp * 256] = (unsigned short)(far0 ? c0 : c1);
+            ++sp;
+            node = far0 ? c1 : c0;
+        } else if (h[0]) {
+            node = c0;
+        } else if (h[1]) {
+            node = c1;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            node = stk[sp * 256];
+        }
+    }
+}
+
 // closest_hit, main.c:52-92: spheres, then triangles; a strictly closer hit
 // replaces the record.  Returns the winner (kind, index, t).
-template <bool COUNT>
+template <bool COUNT, bool BVH>
 __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const V3 d, double& t_best, int& idx,
                                            Cnt& cnt)
 {
@@ -298,28 +400,11 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
     double best;
     int win = spheres_closest<COUNT>(kp, o, d, two_a, four_a, inv2a, fast, rc2a, best, cnt);
     int kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
-    const TriGeo* __restrict__ tri = kp.tri;
-    for (int k = 0; k < kp.nt; ++k) {                     // hit_triangle, mesh.h:70-94
-        const TriGeo g = tri[k];
-        const double det = -(d.x * g.nx + d.y * g.ny + d.z * g.nz);
-        if (det >= 1E-6) {
-            const V3 ao = v3(o.x - g.ax, o.y - g.ay, o.z - g.az);
-            const V3 dao = cross(ao, d);
-            double invDet;
-            if (det <= 0x1p400) invDet = div_core(1.0, det, rcp_refined(det));   // det >= 1e-6: exact
-            else invDet = 1 / det;
-            const double dst = (ao.x * g.nx + ao.y * g.ny + ao.z * g.nz) * invDet;
-            if (dst >= 0.0000001 && dst < best) {
-                const double u = (g.acx * dao.x + g.acy * dao.y + g.acz * dao.z) * invDet;
-                const double v = -(g.abx * dao.x + g.aby * dao.y + g.abz * dao.z) * invDet;
-                const double w = 1 - u - v;
-                if (u >= 0.0000001 && v >= 0.0000001 && w >= 0.0000001) {
-                    best = dst;
-                    kind = HIT_TRI;
-                    win = k;
-                }
-            }
-        }
+    int win_orig = 0;
+    if (BVH) {
+        tris_bvh<COUNT>(kp, o, d, best, kind, win, win_orig, cnt);
+    } else {
+        for (int k = 0; k < kp.nt; ++k) tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
     }
     t_best = best;
     idx = win;
@@ -436,7 +521,7 @@ __device__ __forceinline__ V3 hsl_roundtrip(V3 rgb)
 }
 
 // ambient_occlusion, main.c:94-116: one cast, only distance/dst matters.
-template <bool COUNT>
+template <bool COUNT, bool BVH>
 __device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const V3 n, double AO, Stream& st,
                                             Cnt& cnt)
 {
@@ -444,7 +529,7 @@ __device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const
     const V3 dir = normalize(n + rd);
     double t;
     int idx;
-    const int kind = closest_hit<COUNT>(kp, p, dir, t, idx, cnt);
+    const int kind = closest_hit<COUNT, BVH>(kp, p, dir, t, idx, cnt);
     double occ = 0.0;
     if (kind != HIT_NONE) {
         const V3 hp = p + muls(dir, t);
@@ -468,7 +553,7 @@ __device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const
 // i == alpha_depth, i.e. along the primary chain of consecutive alpha holes,
 // and the next chain bounce always overwrites them; they are final when the
 // chain ends (first non-hole bounce, a miss, a light, or the last bounce).
-template <bool COUNT>
+template <bool COUNT, bool BVH>
 __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, Stream& st, double* acc, Cnt& cnt)
 {
     V3 inc = v3(0, 0, 0), rc = v3(1, 1, 1);
@@ -481,7 +566,7 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, 
     for (int i = 0; i < kp.B; i++) {
         double t;
         int idx;
-        const int kind = closest_hit<COUNT>(kp, o, d, t, idx, cnt);
+        const int kind = closest_hit<COUNT, BVH>(kp, o, d, t, idx, cnt);
         V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0);
         Mat mat = Mat{v3(0, 0, 0), v3(0, 0, 0), 0.0, 0.0, 0.0, 0.0};
         if (kind == HIT_SPHERE) {
@@ -547,7 +632,7 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, 
             inc = inc + mulv(em, rc);
             if (rc.x > 0.5 || rc.y > 0.5 || rc.z > 0.5) rc = mulv(mat.diff, muls(rc, 1.3));
             rc = mulv(mat.diff, rc);
-            const double occ = ao_factor<COUNT>(kp, hp, hn, AO, st, cnt);
+            const double occ = ao_factor<COUNT, BVH>(kp, hp, hn, AO, st, cnt);
             rc = mulv(rc, v3(occ, occ, occ));
         } else {
             const V3 em = muls(mat.emis, mat.es);
@@ -585,7 +670,7 @@ __device__ __forceinline__ void write_pixel(const KParams& kp, long long li, V3 
 }
 
 // fill_canva, main.c:245-284: thread = (pixel, chunk of its samples).
-template <bool COUNT>
+template <bool COUNT, bool BVH>
 __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KParams kp)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -631,7 +716,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KP
             const V3 dest = co + muls(dir, U[b + U_FOCUS]);
             const V3 no = co + v3(dx, dy, 0);
             const V3 rd = normalize(dest - no);
-            trace<COUNT>(kp, no, rd, U[b + U_AO], st, acc, cnt);
+            trace<COUNT, BVH>(kp, no, rd, U[b + U_AO], st, acc, cnt);
             if (COUNT) {
                 cnt.c[RT_CNT_SAMPLES] += 1;
                 cnt.c[RT_CNT_RNG_DRAWS] += st.n;
@@ -767,7 +852,10 @@ static dim3 grid_for(const KParams& kp)
 
 int launch_render(const KParams& kp, void* stream)
 {
-    hipLaunchKernelGGL(render_kernel<false>, grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
+    if (kp.bvh)
+        hipLaunchKernelGGL((render_kernel<false, true>), grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
+    else
+        hipLaunchKernelGGL((render_kernel<false, false>), grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
     if (kp.chunks > 1) {
         const long long npx = (long long)kp.local_rows * kp.W;
         long long blocks = (npx + 255) / 256;
@@ -779,7 +867,10 @@ int launch_render(const KParams& kp, void* stream)
 
 int launch_count(const KParams& kp, void* stream)
 {
-    hipLaunchKernelGGL(render_kernel<true>, grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
+    if (kp.bvh)
+        hipLaunchKernelGGL((render_kernel<true, true>), grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
+    else
+        hipLaunchKernelGGL((render_kernel<true, false>), grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
     return (int)hipGetLastError();
 }
 

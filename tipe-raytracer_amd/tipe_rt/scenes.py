@@ -88,3 +88,47 @@ def load_mesh_fixture(name):
         # are never written by the reference loader (read as 0).
         mats[k] = material((r, g, b), BLACK, 0.0, 0.0, a, 0.0)
     return arr, qm, mats, d["tex_width"], d["tex_height"], d["n_materials"]
+
+
+# Scene placements (SURVEY.md §8 "Config resolution").
+PYRAMID_MOVE = (-0.6, -1.0, -2.0)    # C3/C5: probe-verified on the floor
+TREE_MOVE = (0.3, -1.01, -2.1)       # C4: the CUDA loader's displacement, triangle.hu:87
+
+
+def moved(mesh, delta):
+    """move_mesh (mesh.h:220-234): add delta to every vertex, in place."""
+    tris = mesh[0]
+    for t in tris:
+        for P in (t.A, t.B, t.C):
+            P.e[0] += delta[0]
+            P.e[1] += delta[1]
+            P.e[2] += delta[2]
+    return mesh
+
+
+def load_tree_fixture():
+    """tests/golden/scenes/tree.json (tests/golden/make_tree_fixture.py):
+    1tree_tri.obj through librt_host.so, Kd-flat 1x1 texels with
+    reflectionStrength = Ns/100.  Same tuple as load_mesh_fixture."""
+    with open(os.path.join(_GOLDEN, "scenes", "tree.json")) as f:
+        d = json.load(f)
+    tris = d["triangles"]
+    arr = (Triangle * len(tris))()
+    for k, t in enumerate(tris):
+        arr[k].A, arr[k].B, arr[k].C = Vec3(*t[0:3]), Vec3(*t[3:6]), Vec3(*t[6:9])
+        arr[k].mat = material(SKY, BLACK, 0.0, 0.0, 0.0, 0.0)
+    qm = (C.c_int * len(tris))(*d["quelMatPourTri"])
+    mats = (Material * len(d["texels"]))()
+    for k, (r, g, b, a, refl) in enumerate(d["texels"]):
+        mats[k] = material((r, g, b), BLACK, 0.0, refl, a, 0.0)
+    return arr, qm, mats, d["tex_width"], d["tex_height"], d["n_materials"]
+
+
+def pyramid_mesh():
+    """C3/C5 mesh: pyramide_tri.obj (reference loader output) at PYRAMID_MOVE."""
+    return moved(load_mesh_fixture("pyramide"), PYRAMID_MOVE)
+
+
+def tree_mesh():
+    """C4 mesh: 1tree_tri.obj (1320 tris) at TREE_MOVE."""
+    return moved(load_tree_fixture(), TREE_MOVE)

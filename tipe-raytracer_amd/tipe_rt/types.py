@@ -7,9 +7,12 @@ RT_RNG_PHILOX, RT_RNG_GLIBC = 0, 1
 
 (RT_CNT_SAMPLES, RT_CNT_CASTS, RT_CNT_SPHERE_TESTS, RT_CNT_SPHERE_DISC,
  RT_CNT_TRI_TESTS, RT_CNT_SHADE, RT_CNT_TEX_HITS, RT_CNT_REFRACT,
- RT_CNT_RNG_DRAWS, RT_CNT_EXACT_RESCANS, RT_NCOUNTERS) = range(11)
+ RT_CNT_RNG_DRAWS, RT_CNT_EXACT_RESCANS, RT_CNT_BVH_NODES, RT_CNT_BVH_TRI_TESTS,
+ RT_NCOUNTERS) = range(13)
 COUNTER_NAMES = ["samples", "casts", "sphere_tests", "sphere_disc", "tri_tests",
-                 "shade", "tex_hits", "refract", "rng_draws", "exact_rescans"]
+                 "shade", "tex_hits", "refract", "rng_draws", "exact_rescans",
+                 "bvh_nodes", "bvh_tri_tests"]
+RT_ACCEL_AUTO, RT_ACCEL_NONE = 0, 1
 
 
 class Vec3(C.Structure):
@@ -89,7 +92,7 @@ class Params(C.Structure):
                 ("ouverture_x", C.c_double), ("ouverture_y", C.c_double),
                 ("AO_intensity", C.c_double), ("useAO", C.c_int),
                 ("compat_int_truncation", C.c_int), ("rng", C.c_int),
-                ("spp_chunks", C.c_int), ("seed", C.c_ulonglong)]
+                ("spp_chunks", C.c_int), ("seed", C.c_ulonglong), ("accel", C.c_int)]
 
 
 class Tiling(C.Structure):

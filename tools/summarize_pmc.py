@@ -25,6 +25,13 @@ s = {c: per_dispatch("sq", c) for c in ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_S
                                        "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"]}
 s.update({c: per_dispatch("sq2", c) for c in ["SQ_ACTIVE_INST_VALU", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY",
                                              "SQ_ACTIVE_INST_ANY", "GRBM_GUI_ACTIVE"]})
+mix = {c: per_dispatch("mix", c) for c in ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                           "SQ_INSTS_VALU_TRANS_F64", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64",
+                                           "SQ_INSTS_VALU_CVT", "SQ_INSTS_BRANCH"]}
+fl = {c: per_dispatch("flops", c) for c in ["SQ_INSTS_VALU_FLOPS_FP64", "SQ_INSTS_VALU_FLOPS_FP64_TRANS",
+                                           "SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"]}
+s.update({k: v for k, v in mix.items() if v is not None})
+s.update({k + ("@flops_pass" if k == "SQ_ACTIVE_INST_VALU" else ""): v for k, v in fl.items() if v is not None})
 dur_ns = float(render["AverageNs"])
 out = {"kernel": render["Name"], "calls": int(render["Calls"]), "avg_ms": dur_ns / 1e6,
        "fetch_kib_raw": fetch_kib, "write_kib": write_kib,
@@ -33,12 +40,16 @@ out = {"kernel": render["Name"], "calls": int(render["Calls"]), "avg_ms": dur_ns
        "valu_active_frac_of_wave_cycles": s["SQ_ACTIVE_INST_VALU"] / s["SQ_WAVE_CYCLES"] if s["SQ_WAVE_CYCLES"] else None,
        "wait_any_frac": s["SQ_WAIT_ANY"] / s["SQ_WAVE_CYCLES"] if s["SQ_WAVE_CYCLES"] else None,
        "wait_inst_any_frac": s["SQ_WAIT_INST_ANY"] / s["SQ_WAVE_CYCLES"] if s["SQ_WAVE_CYCLES"] else None,
+       "valu_lane_utilization": (fl["SQ_THREAD_CYCLES_VALU"] / (fl["SQ_ACTIVE_INST_VALU"] * 64)
+                                 if fl["SQ_THREAD_CYCLES_VALU"] and fl["SQ_ACTIVE_INST_VALU"] else None),
+       "hw_fp64_tflops": (fl["SQ_INSTS_VALU_FLOPS_FP64"] / (dur_ns * 1e-9) / 1e12
+                          if fl["SQ_INSTS_VALU_FLOPS_FP64"] else None),
        "note": "FETCH_SIZE doubled (gfx950 reports half of wide-load bytes, MI355X_MICROARCH.md HBM); "
                "units KiB; per render_kernel<false> launch; PMC runs are separate rocprofv3 passes"}
 json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
 for f in ["kt/run_kernel_stats.csv"]:
     os.system("cp %s %s" % (os.path.join(src, f), os.path.join(dst, "kernel_stats.csv")))
-for d in ["fetch", "write", "sq", "sq2"]:
+for d in ["fetch", "write", "sq", "sq2", "mix", "flops"]:
     p = os.path.join(src, d, "run_counter_collection.csv")
     if os.path.exists(p):
         os.system("cp %s %s" % (p, os.path.join(dst, "pmc_%s.csv" % d)))
