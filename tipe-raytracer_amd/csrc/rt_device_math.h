@@ -96,7 +96,15 @@ struct Stream {
     __device__ __forceinline__ uint32_t next31()
     {
         const uint32_t slot = n & 3u;
-        if (slot == 0u) blk = philox4x32_10(n >> 2, 0u, pixel, sample, k0, k1);
+        if (slot == 0u) {
+            blk = philox4x32_10(n >> 2, 0u, pixel, sample, k0, k1);
+#ifdef RT_DUP_PHILOX
+            uint32_t m = 0, px2 = pixel;
+            asm volatile("" : "+v"(m), "+v"(px2));
+            const Philox b2 = philox4x32_10(n >> 2, 0u, px2, sample, k0, k1);
+            blk.w0 ^= (b2.w0 ^ b2.w1 ^ b2.w2 ^ b2.w3) & m;
+#endif
+        }
         const uint32_t w = slot == 0u ? blk.w0 : slot == 1u ? blk.w1 : slot == 2u ? blk.w2 : blk.w3;
         ++n;
         return w >> 1;

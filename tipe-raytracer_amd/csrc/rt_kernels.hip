@@ -49,6 +49,9 @@
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
+#ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
+#define RT_WAVES_PER_SIMD_BVH 3
+#endif
 
 namespace rt {
 
@@ -115,6 +118,22 @@ __device__ __forceinline__ V3 normalize(V3 a)
     return divs(a, sqrt(n2));
 }
 
+// Cost-attribution knobs (tools/attribute_costs.sh): RT_DUP_<part> runs a
+// part twice on opaque copies of its inputs and keeps the first result, so
+// the measured slowdown is that part's cost.  Off in every shipped build.
+__device__ __forceinline__ bool opaque_false()
+{
+    int z = 0;
+    asm volatile("" : "+v"(z));
+    return z != 0;
+}
+template <class T>
+__device__ __forceinline__ T launder(T x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 struct Mat {
     V3 diff, emis;
     double es, rs, alpha, ior;
@@ -129,12 +148,50 @@ __device__ __forceinline__ Mat load_mat(const DevMat* m)
 // per thread ([9][256], conflict-free), so they occupy no VGPRs across the
 // bounce loop.  Only the owning thread touches its column: plain
 // read-add-write, same IEEE adds in the same order as fill_canva's sums.
+__device__ __forceinline__ V3 lds_get(const double* acc, int base)
+{
+    return v3(acc[(base + 0) * 256], acc[(base + 1) * 256], acc[(base + 2) * 256]);
+}
+__device__ __forceinline__ void lds_put(double* acc, int base, V3 v)
+{
+    acc[(base + 0) * 256] = v.x;
+    acc[(base + 1) * 256] = v.y;
+    acc[(base + 2) * 256] = v.z;
+}
 __device__ __forceinline__ void acc_add(double* acc, int base, V3 v)
 {
     acc[(base + 0) * 256] = acc[(base + 0) * 256] + v.x;
     acc[(base + 1) * 256] = acc[(base + 1) * 256] + v.y;
     acc[(base + 2) * 256] = acc[(base + 2) * 256] + v.z;
 }
+
+enum : int { ACC_RAD = 0, ACC_ALB = 3, ACC_NRM = 6, ACC_INC = 9, ACC_RC = 12, ACC_SLOTS = 15 };
+
+// incomingLight / rayColor of tracer (main.c:124-125).  In LDS slots 9..14
+// for the sphere kernel (touched once per bounce, frees 12 VGPRs across the
+// hit scans); in registers for the BVH kernel, whose LDS budget goes to the
+// traversal stack (4 blocks/CU need <= 40 KB each).
+template <bool IN_LDS>
+struct PathState;
+template <>
+struct PathState<true> {
+    double* acc;
+    __device__ void init() { lds_put(acc, ACC_INC, v3(0, 0, 0)); lds_put(acc, ACC_RC, v3(1, 1, 1)); }
+    __device__ V3 inc() const { return lds_get(acc, ACC_INC); }
+    __device__ V3 rc() const { return lds_get(acc, ACC_RC); }
+    __device__ void set_inc(V3 v) { lds_put(acc, ACC_INC, v); }
+    __device__ void set_rc(V3 v) { lds_put(acc, ACC_RC, v); }
+};
+template <>
+struct PathState<false> {
+    double* acc;
+    V3 i_, r_;
+    __device__ void init() { i_ = v3(0, 0, 0); r_ = v3(1, 1, 1); }
+    __device__ V3 inc() const { return i_; }
+    __device__ V3 rc() const { return r_; }
+    __device__ void set_inc(V3 v) { i_ = v; }
+    __device__ void set_rc(V3 v) { r_ = v; }
+};
 
 // Per-thread event counters (COUNT instantiation only).
 struct Cnt {
@@ -183,12 +240,12 @@ __device__ __forceinline__ bool sphere_exact(double cx, double cy, double cz, do
 // Closest sphere (main.c:59-78).  Candidate pass with error intervals, then
 // the exact test for the winner; exact scan on any ambiguity.
 //
-// Interval bound (DESIGN.md "Exact closest hit"): sa = disc*r1 with r1 one
-// Newton step from v_rsq_f64 has |sa/sqrt(disc) - 1| <= 2^-45 (measured
-// 2^-47.7 over 1e9 inputs; v_rsq_f64 <= 2^-24.2), so with q = RN(n_a*inv2a)
-// the exact root t satisfies |t - q| <= sa*inv2a*2^-39.7 + |q|*2^-50; the
-// margin used, sa*inv2a*2^-39 + |q|*2^-49, also absorbs the rounding of the
-// interval end points.
+// Interval bound (DESIGN.md "Exact closest hit"): sa, one Newton step from
+// v_rsq_f64, has |sa/sqrt(disc) - 1| <= 2^-45 (measured 2^-47.7 over 1e9
+// inputs; v_rsq_f64 <= 2^-24.2), so with q = RN(n_a*inv2a) the exact root t
+// satisfies |t - q| <= sa*inv2a*2^-39.7 + |q|*2^-50 < (|b| + sa)*inv2a*2^-39
+// (|q| <= (|b| + sa)*inv2a); the margin used, M = (|b| + sa)*inv2a*2^-38,
+// also absorbs the rounding of M and of the interval end points.
 template <bool COUNT>
 __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, const V3 d, double two_a,
                                                double four_a, double inv2a, bool fast, double rc2a,
@@ -199,6 +256,7 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     double blo = INF, bhi = INF;
     int bk = -1;
     bool amb = false;
+    const double inv2a_m = inv2a * 0x1p-38;
     for (int k = 0; k < kp.ns_pad; k += 2) {
         double g[8];
 #pragma unroll
@@ -215,39 +273,33 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
                     amb = true;
                     continue;
                 }
+                // sa ~ sqrt(disc): v_rsq_f64 + one Newton step folded into
+                // sa = t + t*e/2, t = disc*r0, e = 1 - t*r0 (fma).
                 const double r0 = __builtin_amdgcn_rsq(disc);
-                const double r1 = r0 * (1.5 - (0.5 * disc) * (r0 * r0));
-                const double sa = disc * r1;
-                const double sm = (sa * inv2a) * 0x1p-39;
-                double lo = 0.0, hi = 0.0;
-                bool cand = false;
-                const double q1 = (-b - sa) * inv2a;
-                const double m1 = sm + fabs(q1) * 0x1p-49;
-                if (q1 - m1 >= 0.0001) {
-                    lo = q1 - m1;
-                    hi = q1 + m1;
-                    cand = true;
-                } else if (q1 + m1 < 0.0001) {
-                    const double q2 = (-b + sa) * inv2a;
-                    const double m2 = sm + fabs(q2) * 0x1p-49;
-                    if (q2 - m2 >= 0.0001) {
-                        lo = q2 - m2;
-                        hi = q2 + m2;
-                        cand = true;
-                    } else if (!(q2 + m2 < 0.0001)) {
+                const double tt = disc * r0;
+                const double sa = fma(tt * 0.5, fma(-tt, r0, 1.0), tt);
+                // one margin for both roots: (|b| + sa)/(2a) * 2^-38 bounds
+                // sa*inv2a*2^-39.7 + |q|*2^-50
+                const double M = (fabs(b) + sa) * inv2a_m;
+                double q = (-b - sa) * inv2a;              // near root t1
+                if (!(q - M >= 0.0001)) {
+                    if (q + M >= 0.0001) {                 // t1 straddles the 1e-4 threshold
                         amb = true;
+                        continue;
                     }
-                } else {
-                    amb = true;
+                    q = (sa - b) * inv2a;                  // far root t2
+                    if (!(q - M >= 0.0001)) {
+                        if (q + M >= 0.0001) amb = true;
+                        continue;
+                    }
                 }
-                if (cand) {
-                    if (hi < blo) {
-                        blo = lo;
-                        bhi = hi;
-                        bk = k + h;
-                    } else if (!(lo >= bhi)) {
-                        amb = true;
-                    }
+                const double lo = q - M, hi = q + M;
+                if (hi < blo) {
+                    blo = lo;
+                    bhi = hi;
+                    bk = k + h;
+                } else if (!(lo >= bhi)) {
+                    amb = true;
                 }
             }
         }
@@ -399,6 +451,16 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
     }
     double best;
     int win = spheres_closest<COUNT>(kp, o, d, two_a, four_a, inv2a, fast, rc2a, best, cnt);
+#ifdef RT_DUP_SPHERES
+    {
+        double b2;
+        const int w2 = spheres_closest<COUNT>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, two_a, four_a,
+                                              inv2a, fast, rc2a, b2, cnt);
+        const bool f = opaque_false();
+        best = f ? b2 : best;
+        win = f ? w2 : win;
+    }
+#endif
     int kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
     int win_orig = 0;
     if (BVH) {
@@ -462,11 +524,29 @@ __device__ __forceinline__ V3 random_dir(Stream& st, Cnt& cnt)
     const double u = unit31(st.next31());
     const double v = unit31(st.next31());
     const double theta = 0x1.921fb54442d18p+2 * u;        // 2*PI*u
-    const double phi = pm_acos(2 * v - 1);
+    double phi = pm_acos(2 * v - 1);
+#ifdef RT_DUP_ACOS
+    { const double p2 = pm_acos(launder(2 * v - 1)); phi = opaque_false() ? p2 : phi; }
+#endif
     float st_, ct_, sp_, cp_;
     pm_sincosf((float)theta, st_, ct_);
     pm_sincosf((float)phi, sp_, cp_);
+#ifdef RT_DUP_SINCOS
+    {
+        float a, b, c2, d2;
+        pm_sincosf(launder((float)theta), a, b);
+        pm_sincosf(launder((float)phi), c2, d2);
+        const bool f = opaque_false();
+        st_ = f ? a : st_; ct_ = f ? b : ct_; sp_ = f ? c2 : sp_; cp_ = f ? d2 : cp_;
+    }
+#endif
     const V3 dir = v3((double)(ct_ * sp_), (double)(st_ * sp_), (double)cp_);
+#ifdef RT_DUP_NORMALIZE
+    {
+        const V3 a = normalize(dir), b = normalize(v3(launder(dir.x), launder(dir.y), launder(dir.z)));
+        return opaque_false() ? b : a;
+    }
+#endif
     return normalize(dir);
 }
 
@@ -556,7 +636,8 @@ __device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const
 template <bool COUNT, bool BVH>
 __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, Stream& st, double* acc, Cnt& cnt)
 {
-    V3 inc = v3(0, 0, 0), rc = v3(1, 1, 1);
+    PathState<!BVH> ps{acc};
+    ps.init();
     bool chain = true;
     double top_n2 = 1.0;
     if (kp.B <= 0) {                                     // tracer returns (0, 0, 0) albedo/normal
@@ -627,21 +708,23 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, 
         } else if (mat.alpha > 0.99) {
             d = dr;
         }
+        V3 rc = ps.rc();
         if (kp.useAO) {
             const V3 em = muls(mat.emis, mat.es * 1.5 * AO);
-            inc = inc + mulv(em, rc);
+            ps.set_inc(ps.inc() + mulv(em, rc));
             if (rc.x > 0.5 || rc.y > 0.5 || rc.z > 0.5) rc = mulv(mat.diff, muls(rc, 1.3));
             rc = mulv(mat.diff, rc);
+            ps.set_rc(rc);
             const double occ = ao_factor<COUNT, BVH>(kp, hp, hn, AO, st, cnt);
-            rc = mulv(rc, v3(occ, occ, occ));
+            ps.set_rc(mulv(ps.rc(), v3(occ, occ, occ)));
         } else {
             const V3 em = muls(mat.emis, mat.es);
-            inc = inc + mulv(em, rc);
+            ps.set_inc(ps.inc() + mulv(em, rc));
             if (rc.x > 0.5 || rc.y > 0.5 || rc.z > 0.5) rc = mulv(mat.diff, muls(rc, 1.3));
-            rc = mulv(mat.diff, rc);
+            ps.set_rc(mulv(mat.diff, rc));
         }
     }
-    acc_add(acc, 0, inc);
+    acc_add(acc, ACC_RAD, ps.inc());
 }
 
 // write_color_canva, rtutility.h:56-71 (sqrtf of the float-rounded product)
@@ -671,7 +754,7 @@ __device__ __forceinline__ void write_pixel(const KParams& kp, long long li, V3 
 
 // fill_canva, main.c:245-284: thread = (pixel, chunk of its samples).
 template <bool COUNT, bool BVH>
-__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KParams kp)
+__global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIMD) void render_kernel(const KParams kp)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
@@ -691,7 +774,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel(const KP
         const uint32_t pixel = (uint32_t)g * (uint32_t)kp.W + (uint32_t)x;
         const int s0 = (int)(((long long)chunk * kp.S) / kp.chunks);
         const int s1 = (int)(((long long)(chunk + 1) * kp.S) / kp.chunks);
-        __shared__ double acc_lds[9 * 256];
+        __shared__ double acc_lds[(BVH ? ACC_INC : ACC_SLOTS) * 256];
         double* acc = acc_lds + threadIdx.x;
 #pragma unroll
         for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
