@@ -67,7 +67,9 @@ def test_device_math_bitexact():
     rng = np.random.default_rng(7)
     n = 4096
     k = rng.integers(0, 2 ** 31, n)
-    xs = np.concatenate([2.0 * (k / 2147483648.0) - 1.0, [-1.0, -0.5, 0.5, 0.0, 1e-20, -1e-300]])
+    edge = [-1.0, -0.5, 0.5, 0.0, 1e-20, -1e-300, 1 - 2.0 ** -53, -1 + 2.0 ** -53, 0.5 - 2.0 ** -54,
+            -0.5 + 2.0 ** -54, 2.0 ** -31, -(2.0 ** -31), 0.9999999999, -0.9999999999]
+    xs = np.concatenate([2.0 * (k / 2147483648.0) - 1.0, rng.uniform(-1, 1, n), edge])
     got = tipe_rt.selftest_math(0, xs, len(xs))
     want = np.array([o.oracle_pm_acos(x) for x in xs])
     assert (got.view(np.uint64) == want.view(np.uint64)).all()

@@ -141,13 +141,46 @@ __device__ __forceinline__ void pm_sincosf(float x, float& sn, float& cs)
     cs = (float)vc;
 }
 
+// Exact f64 sqrt and division without their range fixups.  These are the
+// compiler's own gfx950 lowerings of the IEEE operations -- sqrt: v_rsq +
+// Goldschmidt/Newton (10 ops); x/d: v_div_scale, v_rcp, two Newton steps on
+// the reciprocal, mul, fma, v_div_fmas, v_div_fixup -- with the scaling and
+// special-value steps dropped.  Those steps are identities under the guards
+// each call site checks (no zero/inf/NaN/denormal operand or intermediate,
+// operand exponents well inside the range), so the results are bit-identical
+// to `sqrt` and `/`; lanes outside the guards take the generic operations.
+// The refined reciprocal depends only on the divisor, so one rcp_refined
+// serves every quotient by the same d.  rt_selftest_math op 8 and the parity
+// suite check them.
+__device__ __forceinline__ double sqrt_core(double x)          // x in [2^-760, 2^760]
+{
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    g = fma(fma(-g, g, x), h, g);
+    return fma(fma(-g, g, x), h, g);
+}
+__device__ __forceinline__ double rcp_refined(double d)         // d in [2^-400, 2^400]
+{
+    double rc = __builtin_amdgcn_rcp(d);
+    rc = fma(rc, fma(-d, rc, 1.0), rc);
+    return fma(rc, fma(-d, rc, 1.0), rc);
+}
+__device__ __forceinline__ double div_core(double x, double d, double rc)   // |x| in [2^-900, 2^900]
+{
+    const double q = x * rc;
+    return fma(fma(-d, q, x), rc, q);
+}
+
 // ---- acos (fdlibm scheme) --------------------------------------------------
 __device__ __forceinline__ double pm_acos_R(int b, double z)
 {
     const double p = z * fma(z, fma(z, fma(z, fma(z, fma(z, KCV(b, KC_PS5), KCV(b, KC_PS4)), KCV(b, KC_PS3)),
                                           KCV(b, KC_PS2)), KCV(b, KC_PS1)), KCV(b, KC_PS0));
     const double q = fma(z, fma(z, fma(z, fma(z, KCV(b, KC_QS4), KCV(b, KC_QS3)), KCV(b, KC_QS2)), KCV(b, KC_QS1)), 1.0);
-    return p / q;
+    return div_core(p, q, rcp_refined(q));   // q in [0.7, 1.1], p = +0 or >= 2^-70: exact
 }
 
 __device__ __forceinline__ double pm_acos(double x)
@@ -165,10 +198,16 @@ __device__ __forceinline__ double pm_acos(double x)
     const bool neg = (hx >> 31) != 0;
     const double z = small ? x * x : (neg ? (1.0 + x) * 0.5 : (1.0 - x) * 0.5);
     const double r = pm_acos_R(b, z);
-    const double s = sqrt(z);
+    // The exact unscaled sqrt/division cores apply to every lane whose case
+    // uses them: there z = (1 -+ x)/2 is in [2^-31, 0.25] (|x| < 1 on the
+    // 2^-31 grid; x = -1 takes the override below), so s + df is in
+    // [2^-15, 1] and the numerator is +0 or >= 2^-84 in magnitude.  Lanes of
+    // the |x| < 0.5 case may feed them z = 0 (NaN, unused).
+    const double s = sqrt_core(z);
     // x >= 0.5
     const double df = __longlong_as_double((long long)((unsigned long long)__double_as_longlong(s) & 0xffffffff00000000ull));
-    const double c = fma(-df, df, z) / (s + df);
+    const double sdf = s + df;
+    const double c = div_core(fma(-df, df, z), sdf, rcp_refined(sdf));
     const double res_pos = 2.0 * (df + fma(r, s, c));
     // x <= -0.5
     const double res_neg = PI - 2.0 * (s + fma(r, s, -PIO2_LO));

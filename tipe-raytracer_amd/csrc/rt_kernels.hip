@@ -70,39 +70,6 @@ __device__ __forceinline__ V3 cross(V3 u, V3 v)
     return v3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
 }
 
-// Exact f64 sqrt and division without their range fixups.  These are the
-// compiler's own gfx950 lowerings of the IEEE operations -- sqrt: v_rsq +
-// Goldschmidt/Newton (10 ops); x/d: v_div_scale, v_rcp, two Newton steps on
-// the reciprocal, mul, fma, v_div_fmas, v_div_fixup -- with the scaling and
-// special-value steps dropped.  Those steps are identities under the guards
-// each call site checks (no zero/inf/NaN/denormal operand or intermediate,
-// operand exponents well inside the range), so the results are bit-identical
-// to `sqrt` and `/`; lanes outside the guards take the generic operations.
-// The refined reciprocal depends only on the divisor, so one rcp_refined
-// serves every quotient by the same d.  rt_selftest_math op 8 and the parity
-// suite check them.
-__device__ __forceinline__ double sqrt_core(double x)          // x in [2^-760, 2^760]
-{
-    const double y = __builtin_amdgcn_rsq(x);
-    double g = x * y, h = y * 0.5;
-    const double r = fma(-h, g, 0.5);
-    g = fma(g, r, g);
-    h = fma(h, r, h);
-    g = fma(fma(-g, g, x), h, g);
-    return fma(fma(-g, g, x), h, g);
-}
-__device__ __forceinline__ double rcp_refined(double d)         // d in [2^-400, 2^400]
-{
-    double rc = __builtin_amdgcn_rcp(d);
-    rc = fma(rc, fma(-d, rc, 1.0), rc);
-    return fma(rc, fma(-d, rc, 1.0), rc);
-}
-__device__ __forceinline__ double div_core(double x, double d, double rc)   // |x| in [2^-900, 2^900]
-{
-    const double q = x * rc;
-    return fma(fma(-d, q, x), rc, q);
-}
-
 // normalize(a) = a / sqrt(dot(a, a)), vec3.h:137-139, bit-exact: fast lanes
 // need dot(a,a) in [2^-760, 2^760] and every |component| >= 2^-900 (so zero
 // components, NaN and extreme lengths take the generic path).
