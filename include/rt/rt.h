@@ -182,6 +182,28 @@ int rt_count_async(const rt_device_scene* scene, const rt_params* params,
                    const rt_tiling* tiling, unsigned long long* d_counters,
                    void* hip_stream);
 
+/* ---- denoiser hook (denoiser.h:31-91, called at main.c:455) -------------- */
+/* denoiser()'s signature.  main.c runs it once on the finished frame when
+ * useDenoiser is set; the OIDN library itself is not part of this one. */
+typedef void (*rt_denoise_fn)(int largeur_image, int hauteur_image, rt_color* canva, rt_camera cam,
+                              rt_color* albedo, rt_color* normal);
+/* Installs (NULL clears; default NULL) the hook rt_render_rows calls after it
+ * has written a whole frame (row_hi = H-1, row_lo = 0) including the albedo
+ * and normal planes, on the calling thread, with params->cam. */
+void rt_set_denoise_hook(rt_denoise_fn fn);
+rt_denoise_fn rt_get_denoise_hook(void);
+
+/* The OIDN "RT" filter's buffer formats (denoiser.h:44-60, 80-84): float3
+ * planes color = (float)canva / 255.0f, albedo/normal = (float)value, and
+ * back canva = (int)(color * 255.0f).  Host versions, and a device pack of a
+ * device frame for a GPU denoiser (caller's stream; albedo/normal planes are
+ * skipped when their pointers are NULL). */
+int rt_denoise_pack(int W, int H, const rt_color* canva, const rt_color* albedo, const rt_color* normal,
+                    float* color3, float* albedo3, float* normal3);
+int rt_denoise_unpack(int W, int H, const float* color3, rt_color* canva);
+int rt_denoise_pack_async(int W, int H, const rt_frame* frame, float* color3, float* albedo3, float* normal3,
+                          void* hip_stream);
+
 /* Device-math self test: evaluates one device primitive on n host inputs
  * (synchronous, device 0).  op: 0 acos, 1 sinf, 2 cosf, 3 pow(x, y),
  * 4 sqrt, 5 x/y, 6 sqrtf, 7 philox word (in[0..3] = ctr, in[4..5] = key as

@@ -125,12 +125,15 @@ def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
 
 
 def test_kernel_resource_usage_builds_for_gfx950():
-    """The HIP sources cross-compile for gfx950 with no VGPR spills above
-    the budget recorded in DESIGN.md (build check, no GPU)."""
+    """The HIP sources cross-compile for gfx950 within the VGPR/spill
+    budgets recorded in DESIGN.md (build check, no GPU)."""
     out = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tipe-raytracer_amd"), "resource-usage"],
                          capture_output=True, text=True)
     txt = out.stdout + out.stderr
-    m = re.search(r"render_kernelILb0.*?VGPRs: (\d+).*?VGPRs Spill: (\d+)", txt, re.S)
-    assert m, txt[-2000:]
-    vgprs, spills = int(m.group(1)), int(m.group(2))
-    assert vgprs <= 128 and spills <= 32
+    budgets = {"ILb0ELb0E": (128, 48),    # sphere scenes: 4 waves/SIMD
+               "ILb0ELb1E": (168, 32)}    # BVH scenes: 3 waves/SIMD (LDS stack)
+    for sym, (max_vgpr, max_spill) in budgets.items():
+        m = re.search(r"render_kernel" + sym + r".*?VGPRs: (\d+).*?VGPRs Spill: (\d+)", txt, re.S)
+        assert m, txt[-2000:]
+        vgprs, spills = int(m.group(1)), int(m.group(2))
+        assert vgprs <= max_vgpr and spills <= max_spill, (sym, vgprs, spills)

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -109,6 +110,10 @@ int validate_tiling(const rt_tiling* t)
 }
 
 }  // namespace
+
+namespace {
+std::atomic<rt_denoise_fn> g_denoise{nullptr};
+}
 
 struct rt_device_scene {
     int device = 0;
@@ -582,6 +587,49 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, i
         }
     }
     cleanup();
+    // main.c:455: denoiser() on the finished frame
+    const rt_denoise_fn hook = g_denoise.load();
+    if (hook && row_hi == params->hauteur_image - 1 && row_lo == 0 && albedo && normal)
+        hook(W, params->hauteur_image, canva, params->cam, albedo, normal);
+    return RT_OK;
+}
+
+void rt_set_denoise_hook(rt_denoise_fn fn) { g_denoise.store(fn); }
+rt_denoise_fn rt_get_denoise_hook(void) { return g_denoise.load(); }
+
+int rt_denoise_pack(int W, int H, const rt_color* canva, const rt_color* albedo, const rt_color* normal,
+                    float* color3, float* albedo3, float* normal3)
+{
+    if (W < 1 || H < 1 || !canva || !color3) return fail(RT_EINVAL, "bad denoise_pack arguments");
+    const size_t n = (size_t)W * H;
+    for (size_t i = 0; i < n; ++i)
+        for (int c = 0; c < 3; ++c) {
+            color3[3 * i + c] = (float)canva[i].e[c] / 255.0f;          // denoiser.h:44-48
+            if (albedo && albedo3) albedo3[3 * i + c] = (float)albedo[i].e[c];
+            if (normal && normal3) normal3[3 * i + c] = (float)normal[i].e[c];
+        }
+    return RT_OK;
+}
+
+int rt_denoise_unpack(int W, int H, const float* color3, rt_color* canva)
+{
+    if (W < 1 || H < 1 || !canva || !color3) return fail(RT_EINVAL, "bad denoise_unpack arguments");
+    const size_t n = (size_t)W * H;
+    for (size_t i = 0; i < n; ++i)
+        for (int c = 0; c < 3; ++c) canva[i].e[c] = (int)(color3[3 * i + c] * 255.0f);   // denoiser.h:80-84
+    return RT_OK;
+}
+
+int rt_denoise_pack_async(int W, int H, const rt_frame* frame, float* color3, float* albedo3, float* normal3,
+                          void* hip_stream)
+{
+    if (W < 1 || H < 1 || !frame || !frame->canva || !color3)
+        return fail(RT_EINVAL, "bad denoise_pack_async arguments");
+    const int e = launch_denoise_pack((long long)W * H, (const double*)frame->canva,
+                                      albedo3 ? (const double*)frame->albedo : nullptr,
+                                      normal3 ? (const double*)frame->normal : nullptr, color3, albedo3, normal3,
+                                      hip_stream);
+    if (e) return fail(RT_EDEVICE, "denoise pack launch: %s", hipGetErrorString((hipError_t)e));
     return RT_OK;
 }
 

@@ -895,6 +895,31 @@ __global__ void selftest_kernel(int op, const double* __restrict__ in, double* _
     }
 }
 
+// OIDN input planes from a device frame, denoiser.h:44-60 (IEEE f32 ops).
+__global__ __launch_bounds__(256) void denoise_pack_kernel(long long n, const double* __restrict__ canva,
+                                                           const double* __restrict__ albedo,
+                                                           const double* __restrict__ normal, float* __restrict__ c3,
+                                                           float* __restrict__ a3, float* __restrict__ n3)
+{
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        c3[i] = (float)canva[i] / 255.0f;
+        if (a3) a3[i] = (float)albedo[i];
+        if (n3) n3[i] = (float)normal[i];
+    }
+}
+
+int launch_denoise_pack(long long npx, const double* canva, const double* albedo, const double* normal, float* color3,
+                        float* albedo3, float* normal3, void* stream)
+{
+    const long long n = npx * 3;
+    long long blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(denoise_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n, canva,
+                       albedo ? albedo : nullptr, normal, color3, albedo ? albedo3 : nullptr,
+                       normal ? normal3 : nullptr);
+    return (int)hipGetLastError();
+}
+
 static dim3 grid_for(const KParams& kp)
 {
     return dim3((unsigned)((kp.W + 15) / 16), (unsigned)((kp.local_rows + 15) / 16), (unsigned)kp.chunks);

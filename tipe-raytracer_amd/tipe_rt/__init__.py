@@ -58,6 +58,11 @@ def lib():
         L.rt_assemble_async.argtypes = [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_void_p, C.c_void_p]
         L.rt_selftest_math.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        L.rt_set_denoise_hook.argtypes = [DENOISE_FN]
+        L.rt_get_denoise_hook.restype = C.c_void_p
+        L.rt_denoise_pack.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6
+        L.rt_denoise_unpack.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        L.rt_denoise_pack_async.argtypes = [C.c_int, C.c_int, P(Frame)] + [C.c_void_p] * 4
         _lib = L
     return _lib
 
@@ -65,7 +70,41 @@ def lib():
 EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error", "rt_version",
                     "rt_device_count", "rt_render_rows", "rt_fill_canva", "rt_scene_upload",
                     "rt_scene_release", "rt_render_async", "rt_assemble_async", "rt_count_async",
-                    "rt_selftest_math"]
+                    "rt_selftest_math", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
+                    "rt_denoise_unpack", "rt_denoise_pack_async"]
+
+# rt_denoise_fn (rt.h): denoiser()'s signature, denoiser.h:31
+DENOISE_FN = C.CFUNCTYPE(None, C.c_int, C.c_int, C.c_void_p, Camera, C.c_void_p, C.c_void_p)
+_hook_ref = None
+
+
+def set_denoise_hook(fn):
+    """Install a Python callable fn(W, H, canva_ptr, cam, albedo_ptr,
+    normal_ptr) as the rt_render_rows denoiser hook (None clears it)."""
+    global _hook_ref
+    _hook_ref = DENOISE_FN(fn) if fn is not None else DENOISE_FN()
+    lib().rt_set_denoise_hook(_hook_ref)
+
+
+def denoise_pack(canva, albedo=None, normal=None):
+    """OIDN input planes (denoiser.h:44-60) from host (H, W, 3) frames."""
+    H, W = canva.shape[:2]
+    outs = [np.zeros((H, W, 3), np.float32) for _ in range(3)]
+    ptr = lambda a: None if a is None else np.ascontiguousarray(a).ctypes.data  # noqa: E731
+    keep = [np.ascontiguousarray(x) if x is not None else None for x in (canva, albedo, normal)]
+    check(lib().rt_denoise_pack(W, H, ptr(keep[0]), ptr(keep[1]), ptr(keep[2]),
+                                outs[0].ctypes.data, outs[1].ctypes.data if albedo is not None else None,
+                                outs[2].ctypes.data if normal is not None else None))
+    return outs
+
+
+def denoise_unpack(color3):
+    """canva = (int)(color * 255.0f), denoiser.h:80-84."""
+    H, W = color3.shape[:2]
+    out = np.zeros((H, W, 3))
+    c = np.ascontiguousarray(color3, dtype=np.float32)
+    check(lib().rt_denoise_unpack(W, H, c.ctypes.data, out.ctypes.data))
+    return out
 
 
 def check(rc):
