@@ -87,25 +87,31 @@ __device__ __forceinline__ Philox philox4x32_10(uint32_t c0, uint32_t c1, uint32
 // philox(ctr = {n >> 2, 0, pixel, sample}, key = seed) >> 1   (rt.h)
 struct Stream {
     uint32_t k0, k1, pixel, sample, n;
-    Philox blk;
+    uint32_t* cache;         // current Philox block: 4 words in LDS (stride 256)
 
-    __device__ __forceinline__ void start(uint32_t px, uint32_t s, uint32_t key0, uint32_t key1)
+    __device__ __forceinline__ void start(uint32_t px, uint32_t s, uint32_t key0, uint32_t key1, uint32_t* lds)
     {
-        k0 = key0; k1 = key1; pixel = px; sample = s; n = 0;
+        k0 = key0; k1 = key1; pixel = px; sample = s; n = 0; cache = lds;
     }
     __device__ __forceinline__ uint32_t next31()
     {
         const uint32_t slot = n & 3u;
+        uint32_t w;
         if (slot == 0u) {
-            blk = philox4x32_10(n >> 2, 0u, pixel, sample, k0, k1);
+            Philox blk = philox4x32_10(n >> 2, 0u, pixel, sample, k0, k1);
 #ifdef RT_DUP_PHILOX
             uint32_t m = 0, px2 = pixel;
             asm volatile("" : "+v"(m), "+v"(px2));
             const Philox b2 = philox4x32_10(n >> 2, 0u, px2, sample, k0, k1);
             blk.w0 ^= (b2.w0 ^ b2.w1 ^ b2.w2 ^ b2.w3) & m;
 #endif
+            cache[256] = blk.w1;
+            cache[512] = blk.w2;
+            cache[768] = blk.w3;
+            w = blk.w0;
+        } else {
+            w = cache[slot * 256];
         }
-        const uint32_t w = slot == 0u ? blk.w0 : slot == 1u ? blk.w1 : slot == 2u ? blk.w2 : blk.w3;
         ++n;
         return w >> 1;
     }

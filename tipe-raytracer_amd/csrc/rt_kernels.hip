@@ -742,12 +742,13 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
         const int s0 = (int)(((long long)chunk * kp.S) / kp.chunks);
         const int s1 = (int)(((long long)(chunk + 1) * kp.S) / kp.chunks);
         __shared__ double acc_lds[(BVH ? ACC_INC : ACC_SLOTS) * 256];
+        __shared__ uint32_t rng_lds[4 * 256];
         double* acc = acc_lds + threadIdx.x;
 #pragma unroll
         for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
         for (int s = s0; s < s1; ++s) {
             Stream st;
-            st.start(pixel, (uint32_t)s, kp.key0, kp.key1);
+            st.start(pixel, (uint32_t)s, kp.key0, kp.key1, rng_lds + threadIdx.x);
             const double ju = -0.5 + 1.0 * unit31(st.next31());     // randomDouble(-0.5, 0.5)
             const double jv = -0.5 + 1.0 * unit31(st.next31());
             const double jx = -0.5 + 1.0 * unit31(st.next31());
