@@ -261,13 +261,11 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
                     }
                 }
                 const double lo = q - M, hi = q + M;
-                if (hi < blo) {
-                    blo = lo;
-                    bhi = hi;
-                    bk = k + h;
-                } else if (!(lo >= bhi)) {
-                    amb = true;
-                }
+                const bool closer = hi < blo;             // selects, not branches (fewer phi copies)
+                amb = amb || (!closer && !(lo >= bhi));
+                blo = closer ? lo : blo;
+                bhi = closer ? hi : bhi;
+                bk = closer ? k + h : bk;
             }
         }
     }
