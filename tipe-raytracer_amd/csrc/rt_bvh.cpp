@@ -4,7 +4,8 @@
 //
 // Binary BVH, binned SAH (16 bins on the widest centroid axis), leaves of at
 // most 4 triangles (more only at the depth cap).  Each node stores the boxes
-// of BOTH children, so one 128-byte node fetch decides both descents.  Node 0
+// of BOTH children (float, rounded outward), so one 64-byte node fetch
+// decides both descents.  Node 0
 // is the root split; triangles are reordered into leaf order and the kernel
 // keeps each one's original index for the reference's tie-break.
 //
@@ -71,6 +72,18 @@ struct Ref {
 };
 
 constexpr int kLeaf = 4;
+
+// Outward rounding of a double bound to float.
+float down(double x)
+{
+    float f = (float)x;
+    return (double)f > x ? std::nextafter(f, -HUGE_VALF) : f;
+}
+float up(double x)
+{
+    float f = (float)x;
+    return (double)f < x ? std::nextafter(f, HUGE_VALF) : f;
+}
 constexpr int kBins = 16;
 
 struct Builder {
@@ -162,8 +175,8 @@ struct Builder {
         const Ref* ch[2] = {&L, &R};
         for (int c = 0; c < 2; ++c) {
             for (int a = 0; a < 3; ++a) {
-                nd.lo[c][a] = ch[c]->box.lo[a];
-                nd.hi[c][a] = ch[c]->box.hi[a];
+                nd.lo[c][a] = down(ch[c]->box.lo[a]);
+                nd.hi[c][a] = up(ch[c]->box.hi[a]);
             }
             nd.child[c] = ch[c]->index;
             nd.count[c] = ch[c]->leaf ? ch[c]->count : 0;

@@ -9,17 +9,18 @@ namespace rt {
 
 constexpr int kMaxDepth = 30;       // the kernel's LDS stack holds kMaxDepth + 1 entries
 
-// One internal node: the padded boxes of both children (one 128-byte fetch
-// per visit).  count[c] > 0: child c is a leaf of count[c] triangles starting
-// at child[c] (leaf order); count[c] == 0: child[c] is a node index.
+// One internal node: the padded boxes of both children (one 64-byte fetch
+// per visit).  Bounds are the padded double boxes rounded OUTWARD to float
+// (storage only: the slab test runs in double), so every float box contains
+// its double box.  count[c] > 0: child c is a leaf of count[c] triangles
+// starting at child[c] (leaf order); count[c] == 0: child[c] is a node index.
 struct BvhNode {
-    double lo[2][3];
-    double hi[2][3];
+    float lo[2][3];
+    float hi[2][3];
     int child[2];
     int count[2];
-    double pad[2];
 };
-static_assert(sizeof(BvhNode) == 128, "BvhNode");
+static_assert(sizeof(BvhNode) == 64, "BvhNode");
 
 struct BvhBuild {
     std::vector<BvhNode> nodes;     // node 0 = root split

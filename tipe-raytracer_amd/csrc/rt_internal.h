@@ -9,7 +9,7 @@
 //   DevMat  [ns]     80 B  sphere material — gathered for the winner only
 //   TriGeo  [nt]     96 B  A, B-A, C-A, N  — scanned wave-uniformly
 //   TriTex  [nt]    104 B  B, C, uvA/B/C, material — winner only
-//   BvhNode [nodes] 128 B  both child boxes (rt_bvh.h) when nt > 32; the
+//   BvhNode [nodes]  64 B  both child boxes (rt_bvh.h) when nt > 32; the
 //   int     [nt]           triangle arrays are then in leaf order and
 //                          tri_orig maps back to the caller's order
 //   DevMat  [nm*th*tw]     texel table (reference `material` records)

@@ -331,7 +331,7 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
 }
 
 // Triangle BVH traversal (rt_bvh.h layout; host build rt_bvh.cpp).  One
-// 128-byte node holds both child boxes; leaf children are tested on the
+// 64-byte node holds both child boxes (float storage, double slab math); leaf children are tested on the
 // spot, a doubly-hit pair descends into the nearer box and pushes the other
 // on a per-lane LDS stack ([depth][256] uint16, conflict-free).  A box is
 // skipped only when no triangle in it can win or tie (rt_bvh.cpp): the ray
@@ -358,9 +358,9 @@ __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3
         double tn[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
-            const double x0 = (nd->lo[c][0] - o.x) * ix, x1 = (nd->hi[c][0] - o.x) * ix;
-            const double y0 = (nd->lo[c][1] - o.y) * iy, y1 = (nd->hi[c][1] - o.y) * iy;
-            const double z0 = (nd->lo[c][2] - o.z) * iz, z1 = (nd->hi[c][2] - o.z) * iz;
+            const double x0 = ((double)nd->lo[c][0] - o.x) * ix, x1 = ((double)nd->hi[c][0] - o.x) * ix;
+            const double y0 = ((double)nd->lo[c][1] - o.y) * iy, y1 = ((double)nd->hi[c][1] - o.y) * iy;
+            const double z0 = ((double)nd->lo[c][2] - o.z) * iz, z1 = ((double)nd->hi[c][2] - o.z) * iz;
             const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
             const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
             h[c] = tmin <= tmax && tmax >= -sabs && tmin <= best * srel + sabs;
@@ -430,6 +430,17 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
     int win_orig = 0;
     if (BVH) {
         tris_bvh<COUNT>(kp, o, d, best, kind, win, win_orig, cnt);
+#ifdef RT_DUP_TRIS
+        {
+            double b2 = best;
+            int k2 = kind, w2 = win, o2 = win_orig;
+            tris_bvh<COUNT>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2, cnt);
+            const bool f = opaque_false();
+            best = f ? b2 : best;
+            kind = f ? k2 : kind;
+            win = f ? w2 : win;
+        }
+#endif
     } else {
         for (int k = 0; k < kp.nt; ++k) tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
     }
