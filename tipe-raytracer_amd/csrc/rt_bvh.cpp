@@ -25,6 +25,7 @@
 // first-order bounds (3-term dot/cross products, one division).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -71,7 +72,7 @@ struct Ref {
     Box box;
 };
 
-constexpr int kLeaf = 4;
+int kLeaf = 2;                // leaf size target (RT_BVH_LEAF overrides, for tuning; 1-2 measured best)
 
 // Outward rounding of a double bound to float.
 float down(double x)
@@ -192,6 +193,7 @@ double norm3(double x, double y, double z) { return std::sqrt(x * x + y * y + z 
 bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
 {
     out = BvhBuild();
+    if (const char* e = std::getenv("RT_BVH_LEAF")) kLeaf = std::max(1, std::min(16, std::atoi(e)));
     if (nt <= kLeaf) return false;
     double maxN = 0.0;
     std::vector<Prim> P((size_t)nt);
