@@ -124,7 +124,7 @@ struct rt_device_scene {
     TriGeo* tri = nullptr;
     TriTex* tri_tex = nullptr;
     DevMat* texels = nullptr;
-    BvhNode* bvh = nullptr;          // null: no BVH (few triangles)
+    BvhNode4* bvh = nullptr;         // 4-wide BVH; null: no BVH (few triangles)
     int* tri_orig = nullptr;         // leaf order -> caller's triangle index
     int bvh_nodes = 0, bvh_depth = 0;
     double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0;
@@ -421,14 +421,14 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->tw = scene->nbTriangles > 0 ? scene->tex_width : 1;
     ds->th = scene->nbTriangles > 0 ? scene->tex_height : 1;
     ds->n_texels = n_texels;
-    ds->bvh_nodes = (int)bvh.nodes.size();
-    ds->bvh_depth = bvh.depth;
+    ds->bvh_nodes = (int)bvh.nodes4.size();
+    ds->bvh_depth = bvh.depth4;
     ds->s_rel = bvh.s_rel;
     ds->s_abs = bvh.s_abs;
     ds->r_scene = bvh.r_scene;
     if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
         (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels)) ||
-        (rc = upload(&ds->bvh, bvh.nodes)) || (rc = upload(&ds->tri_orig, bvh.order))) {
+        (rc = upload(&ds->bvh, bvh.nodes4)) || (rc = upload(&ds->tri_orig, bvh.order))) {
         free_scene(ds);
         return rc;
     }

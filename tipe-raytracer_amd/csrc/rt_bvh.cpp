@@ -188,6 +188,66 @@ struct Builder {
 
 double norm3(double x, double y, double z) { return std::sqrt(x * x + y * y + z * z); }
 
+// Collapse of the binary tree into 4-wide nodes: a node's children are its
+// binary children, with the internal child of largest box area replaced by
+// its own two children while fewer than four.  Boxes are copied (already
+// rounded outward).
+struct Elem {
+    float lo[3], hi[3];
+    int ref, count;          // count 0: binary node index
+};
+
+float area(const Elem& e)
+{
+    const float x = e.hi[0] - e.lo[0], y = e.hi[1] - e.lo[1], z = e.hi[2] - e.lo[2];
+    return x * y + y * z + z * x;
+}
+
+Elem elem_of(const BvhNode& n, int c)
+{
+    Elem e;
+    for (int a = 0; a < 3; ++a) {
+        e.lo[a] = n.lo[c][a];
+        e.hi[a] = n.hi[c][a];
+    }
+    e.ref = n.child[c];
+    e.count = n.count[c];
+    return e;
+}
+
+int collapse(const std::vector<BvhNode>& bin, int b, std::vector<BvhNode4>& out, int depth, int& max_depth)
+{
+    max_depth = std::max(max_depth, depth);
+    std::vector<Elem> ch = {elem_of(bin[(size_t)b], 0), elem_of(bin[(size_t)b], 1)};
+    while (ch.size() < 4) {
+        int best = -1;
+        for (int i = 0; i < (int)ch.size(); ++i)
+            if (ch[(size_t)i].count == 0 && (best < 0 || area(ch[(size_t)i]) > area(ch[(size_t)best]))) best = i;
+        if (best < 0) break;
+        const BvhNode& n = bin[(size_t)ch[(size_t)best].ref];
+        ch[(size_t)best] = elem_of(n, 0);
+        ch.push_back(elem_of(n, 1));
+    }
+    const int idx = (int)out.size();
+    out.emplace_back();
+    int child[4] = {0, 0, 0, 0}, count[4] = {-1, -1, -1, -1};
+    for (int i = 0; i < (int)ch.size(); ++i) {
+        child[i] = ch[(size_t)i].count > 0 ? ch[(size_t)i].ref
+                                           : collapse(bin, ch[(size_t)i].ref, out, depth + 1, max_depth);
+        count[i] = ch[(size_t)i].count;
+    }
+    BvhNode4& nd = out[(size_t)idx];
+    for (int i = 0; i < 4; ++i) {
+        for (int a = 0; a < 3; ++a) {
+            nd.lo[a][i] = i < (int)ch.size() ? ch[(size_t)i].lo[a] : 0.0f;
+            nd.hi[a][i] = i < (int)ch.size() ? ch[(size_t)i].hi[a] : 0.0f;
+        }
+        nd.child[i] = child[i];
+        nd.count[i] = count[i];
+    }
+    return idx;
+}
+
 }  // namespace
 
 bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
@@ -227,6 +287,11 @@ bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
     out.order.resize((size_t)nt);
     for (int i = 0; i < nt; ++i) out.order[(size_t)i] = P[(size_t)i].idx;
     out.depth = bld.max_depth;
+    collapse(out.nodes, 0, out.nodes4, 0, out.depth4);
+    if (3 * out.depth4 + 1 > kStack4 || out.nodes4.size() >= 65535) {
+        out = BvhBuild();
+        return false;
+    }
     const double k = std::ldexp(1e6, -44) * maxN;
     out.s_rel = k + std::ldexp(1.0, -48);
     out.s_abs = k * r_scene + std::ldexp(r_scene, -48);

@@ -9,7 +9,7 @@
 //   DevMat  [ns]     80 B  sphere material — gathered for the winner only
 //   TriGeo  [nt]     96 B  A, B-A, C-A, N  — scanned wave-uniformly
 //   TriTex  [nt]    104 B  B, C, uvA/B/C, material — winner only
-//   BvhNode [nodes]  64 B  both child boxes (rt_bvh.h) when nt > 32; the
+//   BvhNode4[nodes] 128 B  four child boxes (rt_bvh.h) when nt > 32; the
 //   int     [nt]           triangle arrays are then in leaf order and
 //                          tri_orig maps back to the caller's order
 //   DevMat  [nm*th*tw]     texel table (reference `material` records)
@@ -21,7 +21,7 @@
 
 namespace rt {
 
-struct BvhNode;                                       // rt_bvh.h
+struct BvhNode4;                                      // rt_bvh.h
 
 struct SphGeo { double cx, cy, cz, r2; };            // r2 = radius*radius (sphere.h:22)
 struct DevMat {                                       // == material, hitinfo.h:6-13
@@ -62,7 +62,7 @@ struct KParams {
     const TriTex* tri_tex;
     const DevMat* texels;
     const double* uni;       // U_COUNT doubles
-    const BvhNode* bvh;      // triangle BVH (rt_bvh.h), or null: brute-force scan
+    const BvhNode4* bvh;     // 4-wide triangle BVH (rt_bvh.h), or null: brute-force scan
     const int* tri_orig;     // triangle k's index in the caller's list (null: k)
     double bvh_srel, bvh_sabs;   // distance-cull slack (rt_bvh.cpp)
     int ns, ns_pad, nt;

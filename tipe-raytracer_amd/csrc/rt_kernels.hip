@@ -330,20 +330,21 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
     }
 }
 
-// Triangle BVH traversal (rt_bvh.h layout; host build rt_bvh.cpp).  One
-// 64-byte node holds both child boxes (float storage, double slab math); leaf children are tested on the
-// spot, a doubly-hit pair descends into the nearer box and pushes the other
-// on a per-lane LDS stack ([depth][256] uint16, conflict-free).  A box is
-// skipped only when no triangle in it can win or tie (rt_bvh.cpp): the ray
-// misses the padded box, leaves it behind the origin (tmax < -sabs), or
-// enters it beyond best*(1+srel) + sabs.  Slab reciprocals use |d_i| >=
-// 2^-200, which keeps the products finite without changing any decision
-// for unit-length directions.
+// Triangle BVH traversal (rt_bvh.h: 4-wide nodes collapsed from the binary
+// SAH tree, host build rt_bvh.cpp).  One 128-byte node holds four child
+// boxes (float storage rounded outward; the slab math runs in double); leaf
+// children are tested on the spot, the nearest hit internal child is entered
+// next and the others are pushed on a per-lane LDS stack (uint16
+// [kStack4][256], conflict-free).  A box is skipped only when no triangle in
+// it can win or tie (rt_bvh.cpp): the ray misses the padded box, leaves it
+// behind the origin (tmax < -sabs), or enters it beyond best*(1+srel)+sabs.
+// Slab reciprocals use |d_i| >= 2^-200, which keeps the products finite
+// without changing any decision for unit-length directions.
 template <bool COUNT>
 __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3 d, double& best, int& kind,
                                          int& win, int& win_orig, Cnt& cnt)
 {
-    __shared__ unsigned short stk_lds[(kMaxDepth + 2) * 256];
+    __shared__ unsigned short stk_lds[kStack4 * 256];
     unsigned short* stk = stk_lds + threadIdx.x;
     const double lim = 0x1p-200;
     const double ix = 1.0 / (fabs(d.x) < lim ? copysign(lim, d.x) : d.x);
@@ -352,41 +353,45 @@ __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3
     const double srel = 1.0 + kp.bvh_srel, sabs = kp.bvh_sabs;
     int node = 0, sp = 0;
     while (true) {
-        const BvhNode* nd = kp.bvh + node;
+        const BvhNode4* nd = kp.bvh + node;
         if (COUNT) cnt.c[RT_CNT_BVH_NODES] += 1;
-        bool h[2];
-        double tn[2];
+        bool h[4];
+        double tn[4];
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const double x0 = ((double)nd->lo[c][0] - o.x) * ix, x1 = ((double)nd->hi[c][0] - o.x) * ix;
-            const double y0 = ((double)nd->lo[c][1] - o.y) * iy, y1 = ((double)nd->hi[c][1] - o.y) * iy;
-            const double z0 = ((double)nd->lo[c][2] - o.z) * iz, z1 = ((double)nd->hi[c][2] - o.z) * iz;
+        for (int c = 0; c < 4; ++c) {
+            const double x0 = ((double)nd->lo[0][c] - o.x) * ix, x1 = ((double)nd->hi[0][c] - o.x) * ix;
+            const double y0 = ((double)nd->lo[1][c] - o.y) * iy, y1 = ((double)nd->hi[1][c] - o.y) * iy;
+            const double z0 = ((double)nd->lo[2][c] - o.z) * iz, z1 = ((double)nd->hi[2][c] - o.z) * iz;
             const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
             const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
-            h[c] = tmin <= tmax && tmax >= -sabs && tmin <= best * srel + sabs;
+            h[c] = nd->count[c] >= 0 && tmin <= tmax && tmax >= -sabs && tmin <= best * srel + sabs;
             tn[c] = tmin;
         }
-        const int c0 = nd->child[0], c1 = nd->child[1];
-        const int n0 = nd->count[0], n1 = nd->count[1];
-        if (h[0] && n0 > 0) {
-            for (int k = c0; k < c0 + n0; ++k) tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
-            if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)n0;
-            h[0] = false;
+        int next = -1;
+        double tnext = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (!h[c]) continue;
+            const int ch = nd->child[c], n = nd->count[c];
+            if (n > 0) {
+                for (int k = ch; k < ch + n; ++k) tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
+                if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)n;
+            } else if (next < 0) {
+                next = ch;
+                tnext = tn[c];
+            } else {
+                int push = ch;
+                if (tn[c] < tnext) {                     // nearer: enter it, push the previous pick
+                    push = next;
+                    next = ch;
+                    tnext = tn[c];
+                }
+                stk[sp * 256] = (unsigned short)push;
+                ++sp;
+            }
         }
-        if (h[1] && n1 > 0) {
-            for (int k = c1; k < c1 + n1; ++k) tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
-            if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)n1;
-            h[1] = false;
-        }
-        if (h[0] && h[1]) {
-            const bool far0 = tn[1] < tn[0];
-            stk[sp * 256] = (unsigned short)(far0 ? c0 : c1);
-            ++sp;
-            node = far0 ? c1 : c0;
-        } else if (h[0]) {
-            node = c0;
-        } else if (h[1]) {
-            node = c1;
+        if (next >= 0) {
+            node = next;
         } else {
             if (sp == 0) break;
             --sp;
