@@ -96,17 +96,24 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=12)
-    ap.add_argument("--chunks", type=int, default=int(os.environ.get("RT_BENCH_CHUNKS", "8")),
-                    help="rt_params.spp_chunks (fixed slice grouping of each pixel's samples)")
+    ap.add_argument("--chunks", type=int, default=int(os.environ.get("RT_BENCH_CHUNKS", "32")),
+                    help="rt_params.spp_chunks (fixed slice grouping of each pixel's samples; the same "
+                         "for every N, so the image does not depend on the GPU count)")
+    ap.add_argument("--verify", action="store_true",
+                    help="N>1: rank 0 re-renders the frame alone and checks the assembled planes bit for bit")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: gather through host copies (rehearsing N>1 with all ranks on one GPU); "
+                         "nccl (= RCCL) is the measured configuration")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = local_rank if args.dist_backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local_rank)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
@@ -115,7 +122,7 @@ def main():
     scene = tipe_rt.make_scene(spheres)
     cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
     p = tipe_rt.make_params(W, H, SPP, BOUNCES, cam, focus=3.0, seed=SEED, chunks=args.chunks)
-    ds = tipe_rt.DeviceScene(scene, local_rank)
+    ds = tipe_rt.DeviceScene(scene, gpu)
 
     if world == 1:
         tiling = tipe_rt.band_tiling(0, H - 1)
@@ -134,7 +141,14 @@ def main():
         tipe_rt.render_async(ds, p, tiling, local[0].data_ptr(), local[1].data_ptr(), local[2].data_ptr(),
                              None, sptr)
         if world > 1:
-            dist.gather(local, gather_list, dst=0)     # RCCL over xGMI
+            if args.dist_backend == "nccl":
+                dist.gather(local, gather_list, dst=0)     # RCCL over xGMI
+            else:
+                host = [torch.empty_like(local, device="cpu") for _ in range(world)] if rank == 0 else None
+                dist.gather(local.cpu(), host, dst=0)
+                if rank == 0:
+                    for r in range(world):
+                        gathered[r].copy_(host[r])
             if rank == 0:
                 for pl in range(3):                     # (world, plane, rows, W, 3) -> (plane, H, W, 3)
                     tipe_rt.assemble_async(gathered[0, pl].data_ptr(), world, TILE_ROWS, rows, W, H,
@@ -155,9 +169,19 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    verified = None
+    if args.verify and world > 1 and rank == 0:
+        ref = torch.empty((3, H, W, 3), dtype=torch.float64, device=dev)
+        tipe_rt.render_async(ds, p, tipe_rt.band_tiling(0, H - 1), ref[0].data_ptr(), ref[1].data_ptr(),
+                             ref[2].data_ptr(), None, sptr)
+        torch.cuda.synchronize(dev)
+        verified = bool(torch.equal(ref, full))
+        if not verified:
+            print("verify: assembled frame differs from the single-device frame", file=sys.stderr)
 
     # --- kernel-only timing with HIP events on the launch stream ------------
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -195,6 +219,8 @@ def main():
             "config": {"workload": "C2: 10-sphere Cornell box, 1200x900, 1000 spp, 6 bounces",
                        "width": W, "height": H, "spp": SPP, "bounces": BOUNCES,
                        "tile_rows": TILE_ROWS if world > 1 else H, "parallelism": "row-tiles x%d" % world,
+                       "collective": ("rccl gather" if args.dist_backend == "nccl" else "gloo gather (host)")
+                       if world > 1 else None,
                        "rng": "philox4x32-10", "spp_chunks": args.chunks,
                        "arith": "fp64, reference op order (bit-exact vs oracle)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP64_VECTOR_PEAK_TFLOPS,
@@ -209,6 +235,8 @@ def main():
             "events_per_sample": {k: round(v, 3) for k, v in per.items()},
             "kernel_msamples_per_s": round(launch_samples / (kernel_ms * 1e-3) / 1e6, 3),
         }
+        if verified is not None:
+            rec["verified_vs_single_device"] = verified
         if world == 1 and not args.no_cpu_baseline:
             pc = tipe_rt.make_params(W, H, SPP, BOUNCES, cam, focus=3.0, seed=SEED, chunks=args.chunks)
             rec["cpu_baseline"] = cpu_baseline(pc, scene, threads=args.cpu_threads)
