@@ -224,6 +224,26 @@ def test_bvh_tie_break_on_duplicate_triangles():
     check_parity(bundle, helpers.params(24, 18, 2, 6, accel=1))
 
 
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 5), (5, 1), (2, 2), (17, 3)])
+def test_degenerate_frames(W, H):
+    """largeur_image or hauteur_image of 1 makes main.c:265 divide by zero
+    (u or v = +-inf / nan); the kernel must follow the same IEEE path."""
+    check_parity(helpers.cornell(), helpers.params(W, H, 3, 5))
+
+
+def test_c5_4k_frame_pyramid_one_spp():
+    """C5's 3840x2880 frame (pyramid scene) at 1 spp: 11.06M
+    pixels, pixel indices beyond 2^23, every row of a 4K framebuffer."""
+    bundle = helpers.pyramid_scene()
+    p = helpers.params(3840, 2880, 1, 6)
+    ref = helpers.oracle_render(bundle, p, nthreads=16)
+    canva, alb, nrm, rad = gpu_render(bundle, p)
+    assert_same(canva, ref["canva"], "canva")
+    assert_same(rad, ref["radiance"], "radiance")
+    assert_same(alb, ref["albedo"], "albedo")
+    assert_same(nrm, ref["normal"], "normal")
+
+
 def test_counters_match_oracle():
     import torch
     bundle = helpers.pyramid_scene()
