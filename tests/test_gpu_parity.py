@@ -134,6 +134,13 @@ def test_cornell_spp_chunks_bitexact():
     check_parity(helpers.cornell(), helpers.params(40, 30, 10, 6, chunks=4))
 
 
+def test_spp_chunks_row_bands(monkeypatch):
+    """A partial-sum budget smaller than the frame splits the launch into
+    16-row bands reusing one buffer (rt_api.cpp launch_on_stream): same image."""
+    monkeypatch.setenv("RT_PARTIAL_BUDGET", str(16 * 37 * 4 * 72))     # 16 rows of 37 px x 4 chunks
+    check_parity(helpers.cornell(), helpers.params(37, 53, 8, 5, chunks=4))
+
+
 def test_spp_chunks_only_move_the_last_bits():
     bundle = helpers.cornell()
     a = helpers.oracle_render(bundle, helpers.params(24, 18, 16, 6))

@@ -238,6 +238,15 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
 // Stream-ordered scratch (uniform block, chunk partials) around one launch.
 // The device's default memory pool keeps freed blocks (release threshold
 // raised once), so repeated launches do not re-map memory.
+// Bytes of chunk partials per launch (RT_PARTIAL_BUDGET overrides; tests use
+// a small budget to exercise the banding).
+size_t partial_budget()
+{
+    const char* e = std::getenv("RT_PARTIAL_BUDGET");
+    const long long v = e ? std::atoll(e) : 0;
+    return v > 0 ? (size_t)v : ((size_t)4 << 30);
+}
+
 int launch_on_stream(KParams& kp, const double* uni, hipStream_t st, bool count)
 {
     static std::once_flag pool_once[64];
@@ -258,11 +267,22 @@ int launch_on_stream(KParams& kp, const double* uni, hipStream_t st, bool count)
     UniBlock ub;
     for (int i = 0; i < U_COUNT; ++i) ub.v[i] = uni[i];
     hipError_t e = (hipError_t)launch_set_uniforms(ub, d_uni, st);
-    if (e == hipSuccess && kp.chunks > 1 && !count)
-        e = hipMallocAsync((void**)&d_part, (size_t)kp.chunks * kp.local_rows * kp.W * 9 * sizeof(double), st);
-    if (e == hipSuccess) {
-        kp.uni = d_uni;
-        kp.partial = d_part;
+    // With spp_chunks > 1 the per-chunk partial sums ([chunks][rows*W][9]
+    // doubles) are bounded by kPartialBudget: taller frames are rendered in
+    // row bands that reuse one partial buffer (pixels are independent, so
+    // banding does not change any result).  See partial_budget().
+    int band = kp.local_rows;
+    if (kp.chunks > 1 && !count) {
+        const size_t per_row = (size_t)kp.chunks * kp.W * 9 * sizeof(double);
+        const size_t rows = std::max<size_t>(16, partial_budget() / per_row / 16 * 16);
+        band = (int)std::min<size_t>(rows, (size_t)kp.local_rows);
+        if (e == hipSuccess) e = hipMallocAsync((void**)&d_part, per_row * band, st);
+    }
+    kp.uni = d_uni;
+    kp.partial = d_part;
+    for (int y0 = 0; e == hipSuccess && y0 < kp.local_rows; y0 += band) {
+        kp.band_y0 = y0;
+        kp.band_rows = band;
         e = (hipError_t)(count ? launch_count(kp, st) : launch_render(kp, st));
     }
     if (d_part) (void)hipFreeAsync(d_part, st);

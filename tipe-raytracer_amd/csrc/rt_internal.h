@@ -76,12 +76,13 @@ struct KParams {
     // tiling
     int row_base, tile_rows, tile_first, tile_step, n_tiles, row_end;
     int local_rows;          // n_tiles * tile_rows
+    int band_y0, band_rows;  // local rows [band_y0, band_y0 + band_rows) of this launch (partials are per band)
     // outputs (device, local frame of local_rows x W colors)
     double* canva;
     double* albedo;
     double* normal;
     double* radiance;
-    double* partial;         // chunks > 1: [chunks][local_rows*W][9]
+    double* partial;         // chunks > 1: [chunks][band_rows*W][9]
     unsigned long long* counters;
 };
 

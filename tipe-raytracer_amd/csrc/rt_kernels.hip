@@ -739,12 +739,12 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int ly = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int ly = kp.band_y0 + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
     const int chunk = blockIdx.z;
     Cnt cnt;
     if (COUNT)
         for (int k = 0; k < RT_NCOUNTERS; ++k) cnt.c[k] = 0;
-    bool valid = x < kp.W && ly < kp.local_rows;
+    bool valid = x < kp.W && ly < kp.local_rows && ly < kp.band_y0 + kp.band_rows;
     int g = 0;
     if (valid) {
         const int lt = ly / kp.tile_rows, yy = ly - lt * kp.tile_rows;
@@ -795,7 +795,8 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
             if (kp.chunks == 1) {
                 write_pixel(kp, li, srad, salb, snrm);
             } else {
-                double* p = kp.partial + ((long long)chunk * kp.local_rows * kp.W + li) * 9;
+                double* p = kp.partial + ((long long)chunk * kp.band_rows * kp.W +
+                                          ((long long)(ly - kp.band_y0) * kp.W + x)) * 9;
                 p[0] = srad.x; p[1] = srad.y; p[2] = srad.z;
                 p[3] = salb.x; p[4] = salb.y; p[5] = salb.z;
                 p[6] = snrm.x; p[7] = snrm.y; p[8] = snrm.z;
@@ -814,19 +815,22 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
 // Sum the chunk partials of each pixel in chunk order, then resolve.
 __global__ __launch_bounds__(256) void combine_kernel(const KParams kp)
 {
-    const long long npx = (long long)kp.local_rows * kp.W;
-    for (long long li = (long long)blockIdx.x * blockDim.x + threadIdx.x; li < npx;
-         li += (long long)gridDim.x * blockDim.x) {
-        const int ly = (int)(li / kp.W);
+    const int rows = min(kp.band_rows, kp.local_rows - kp.band_y0);
+    const long long npx = (long long)kp.band_rows * kp.W;      // partial plane stride
+    const long long nb = (long long)rows * kp.W;
+    for (long long bi = (long long)blockIdx.x * blockDim.x + threadIdx.x; bi < nb;
+         bi += (long long)gridDim.x * blockDim.x) {
+        const int ly = kp.band_y0 + (int)(bi / kp.W);
+        const long long li = (long long)kp.band_y0 * kp.W + bi;
         const int lt = ly / kp.tile_rows, yy = ly - lt * kp.tile_rows;
         const int g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + yy;
         if (g >= kp.row_end) continue;
-        const double* p = kp.partial + li * 9;
+        const double* p = kp.partial + bi * 9;
         double a[9];
 #pragma unroll
         for (int j = 0; j < 9; ++j) a[j] = p[j];
         for (int c = 1; c < kp.chunks; ++c) {
-            const double* q = kp.partial + ((long long)c * npx + li) * 9;
+            const double* q = kp.partial + ((long long)c * npx + bi) * 9;
 #pragma unroll
             for (int j = 0; j < 9; ++j) a[j] = a[j] + q[j];
         }
@@ -937,7 +941,7 @@ int launch_denoise_pack(long long npx, const double* canva, const double* albedo
 
 static dim3 grid_for(const KParams& kp)
 {
-    return dim3((unsigned)((kp.W + 15) / 16), (unsigned)((kp.local_rows + 15) / 16), (unsigned)kp.chunks);
+    return dim3((unsigned)((kp.W + 15) / 16), (unsigned)((kp.band_rows + 15) / 16), (unsigned)kp.chunks);
 }
 
 int launch_render(const KParams& kp, void* stream)
@@ -947,7 +951,7 @@ int launch_render(const KParams& kp, void* stream)
     else
         hipLaunchKernelGGL((render_kernel<false, false>), grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
     if (kp.chunks > 1) {
-        const long long npx = (long long)kp.local_rows * kp.W;
+        const long long npx = (long long)kp.band_rows * kp.W;
         long long blocks = (npx + 255) / 256;
         if (blocks > 8192) blocks = 8192;
         hipLaunchKernelGGL(combine_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, kp);
