@@ -1,0 +1,77 @@
+"""Randomised scenes, GPU vs oracle bit for bit (RT_RNG_PHILOX).
+
+Each seed builds a scene the hand-written tests do not: random spheres
+(some enclosing the camera, translucent ones with 1e-4 <= alpha <= 0.99,
+alpha holes, emitters, mirrors), optionally a random textured mesh with
+the reference's hard-coded material overrides (texture.h:71-87, indices
+1/3/4), random camera, aperture, focus, AO on/off, spp_chunks, and more
+than 32 triangles on odd seeds so the BVH path runs.  Sizes stay small
+so the oracle finishes in about a second per scene."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import helpers
+import tipe_rt
+from tipe_rt import scenes
+from tipe_rt.types import Sphere, Triangle, Material, Vec3, UV
+from test_gpu_parity import check_parity
+
+pytestmark = pytest.mark.gpu
+
+
+def random_scene(seed):
+    rng = np.random.default_rng(seed)
+    ns = int(rng.integers(1, 14))
+    sph = (Sphere * ns)()
+    for k in range(ns):
+        kind = rng.choice(["diffuse", "mirror", "glass", "hole", "light", "big"])
+        c = rng.uniform([-2, -2, -6], [2, 2, -1])
+        r = rng.uniform(0.2, 1.2)
+        diff = tuple(rng.uniform(0, 1, 3))
+        em, es, refl, alpha, ior = (0, 0, 0), 0.0, 0.0, 1.0, 1.0
+        if kind == "mirror":
+            refl = float(rng.uniform(0.5, 1.0))
+        elif kind == "glass":
+            alpha, ior = float(rng.uniform(0.05, 0.99)), float(rng.uniform(1.0, 2.0))
+        elif kind == "hole":
+            alpha = 0.0
+        elif kind == "light":
+            em, es = tuple(rng.uniform(0.2, 1, 3)), float(rng.uniform(0.5, 5))
+        elif kind == "big":                               # encloses the camera
+            c, r = rng.uniform(-0.5, 0.5, 3), float(rng.uniform(20, 600))
+        sph[k].center = Vec3(*c)
+        sph[k].radius = r
+        sph[k].mat = scenes.material(diff, em, es, refl, alpha, ior)
+    mesh = None
+    if rng.random() < 0.7:
+        nt = int(rng.integers(40, 120)) if seed % 2 else int(rng.integers(1, 20))
+        tris = (Triangle * nt)()
+        nm, tw, th = 5, int(rng.integers(1, 5)), int(rng.integers(1, 5))
+        qm = (C.c_int * nt)(*[int(x) for x in rng.integers(0, nm, nt)])
+        for k in range(nt):
+            A = rng.uniform([-2, -2, -5], [2, 2, -1.5])
+            e = rng.normal(size=(2, 3)) * 0.5
+            tris[k].A, tris[k].B, tris[k].C = Vec3(*A), Vec3(*(A + e[0])), Vec3(*(A + e[1]))
+            tris[k].uvA, tris[k].uvB, tris[k].uvC = (UV(*rng.uniform(-2, 2, 2)) for _ in range(3))
+        mats = (Material * (nm * tw * th))()
+        for k in range(nm * tw * th):
+            mats[k] = scenes.material(tuple(rng.uniform(0, 1, 3)), (0, 0, 0), 0.0, 0.0,
+                                      float(rng.choice([0.0, 0.5, 1.0, 0.7])), 0.0)
+        mesh = (tris, qm, mats, tw, th, nm)
+    bundle = helpers.SceneBundle(sph, mesh)
+    cam = tipe_rt.init_camera(tuple(rng.uniform(-0.5, 0.5, 3)), tuple(rng.uniform([-1, -1, -4], [1, 1, -2])),
+                              (0, 1, 0), float(rng.uniform(40, 100)), 4.0 / 3.0)
+    W, H = int(rng.integers(8, 33)), int(rng.integers(6, 25))
+    p = helpers.params(W, H, int(rng.integers(1, 6)), int(rng.integers(0, 9)), use_ao=bool(rng.random() < 0.4),
+                       ao=float(rng.uniform(0.5, 3.5)), seed=int(rng.integers(0, 2 ** 40)), cam=cam,
+                       aperture=tuple(rng.choice([0.0, 0.0, 1.0, 2.0], 2)), focus=float(rng.uniform(1, 5)),
+                       compat=int(rng.integers(0, 2)), chunks=int(rng.choice([1, 1, 2, 3])))
+    return bundle, p
+
+
+@pytest.mark.parametrize("seed", range(64))
+def test_random_scene_bitexact(seed):
+    bundle, p = random_scene(seed)
+    check_parity(bundle, p)

@@ -101,6 +101,16 @@ __device__ __forceinline__ T launder(T x)
     return x;
 }
 
+// (int) of a double as the reference's x86-64 build executes it (cvttsd2si):
+// NaN and out-of-range values give INT_MIN, the "integer indefinite".  C
+// leaves this undefined; gfx950's v_cvt_i32_f64 saturates instead (NaN -> 0),
+// so NaN radiance (e.g. AO_intensity truncated to 0, main.c:43/115) would
+// otherwise resolve differently.
+__device__ __forceinline__ int cvt_i32_x86(double x)
+{
+    return (x > -2147483649.0 && x < 2147483648.0) ? (int)x : (int)0x80000000u;
+}
+
 struct Mat {
     V3 diff, emis;
     double es, rs, alpha, ior;
@@ -472,8 +482,8 @@ __device__ __forceinline__ Mat tri_material(const KParams& kp, int k, const V3 P
     v = v - trunc(v);
     if (u < 0) u += 1.0;
     if (v < 0) v += 1.0;
-    const int x = (int)(u * (double)(kp.tw));
-    const int y = (int)(v * (double)(kp.th));
+    const int x = cvt_i32_x86(u * (double)(kp.tw));
+    const int y = cvt_i32_x86(v * (double)(kp.th));
     const int m = tx.mat;
     long long index = ((long long)y * kp.tw + x) + ((long long)kp.th * kp.tw * m);
     index = index < 0 ? 0 : index;                       // reference UB -> clamp
@@ -713,7 +723,7 @@ __device__ __forceinline__ double resolve(double sum, double rapport)
 {
     double r = (double)sqrtf((float)(rapport * sum));
     r = r < 0.0 ? 0.0 : (r > 0.999 ? 0.999 : r);
-    return (double)(int)(256 * r);
+    return (double)cvt_i32_x86(256 * r);
 }
 
 __device__ __forceinline__ void store3(double* base, long long i, V3 v)
