@@ -37,6 +37,10 @@ enum : int {
     KC_SQRT2, KC_L1, KC_L2, KC_L3, KC_L4, KC_L5, KC_L6, KC_L7, KC_L8, KC_L9, KC_L10, KC_L11,
     KC_LN2_HI, KC_LN2_LO, KC_INV_LN2, KC_LN2,
     KC_E2, KC_E3, KC_E4, KC_E5, KC_E6, KC_E7, KC_E8, KC_E9, KC_E10, KC_E11, KC_E12, KC_E13,
+    // tri_uvmapping's per-material overrides (texture.h:71-87) and tracer's
+    // literals: read at the point of use so they are never hoisted into
+    // VGPRs (the compiler spilled them to scratch in every wave's prologue)
+    KC_ES1, KC_A4, KC_IOR4, KC_RS4, KC_A3, KC_IOR3, KC_RS3, KC_THIRD, KC_TWO_THIRDS,
     KC_COUNT
 };
 
@@ -57,6 +61,7 @@ __constant__ const double kC[KC_COUNT] = {
     0x1.0000000000000p-1, 0x1.5555555555555p-3, 0x1.5555555555555p-5, 0x1.1111111111111p-7,
     0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-13, 0x1.a01a01a01a01ap-16, 0x1.71de3a556c734p-19,
     0x1.27e4fb7789f5cp-22, 0x1.ae64567f544e4p-26, 0x1.1eed8eff8d898p-29, 0x1.6124613a86d09p-33,
+    1.85, 0.6, 1.33, 0.93, 0.1, 1.50, 0.3, 1.0 / 3.0, 2.0 / 3.0,
 };
 
 // Scalar load of constant i (index laundered through b = opq0()).

@@ -153,7 +153,14 @@ struct PathState;
 template <>
 struct PathState<true> {
     double* acc;
-    __device__ void init() { lds_put(acc, ACC_INC, v3(0, 0, 0)); lds_put(acc, ACC_RC, v3(1, 1, 1)); }
+    __device__ void init()
+    {
+        // constants materialised here (laundered): hoisted out of the sample
+        // loop they were held in VGPRs and spilled to scratch by every wave
+        const double z = launder(0.0), one = launder(1.0);
+        lds_put(acc, ACC_INC, v3(z, z, z));
+        lds_put(acc, ACC_RC, v3(one, one, one));
+    }
     __device__ V3 inc() const { return lds_get(acc, ACC_INC); }
     __device__ V3 rc() const { return lds_get(acc, ACC_RC); }
     __device__ void set_inc(V3 v) { lds_put(acc, ACC_INC, v); }
@@ -489,20 +496,21 @@ __device__ __forceinline__ Mat tri_material(const KParams& kp, int k, const V3 P
     index = index < 0 ? 0 : index;                       // reference UB -> clamp
     index = index >= kp.n_texels ? kp.n_texels - 1 : index;
     Mat res = load_mat(kp.texels + index);
+    const int b = opq0();
     if (m == 1) {
         res.emis = v3(1, 1, 1);
-        res.es = 1.85;
+        res.es = KCV(b, KC_ES1);          // 1.85
         res.alpha = 1.0;
     }
     if (m == 4) {
-        res.alpha = 0.6;
-        res.ior = 1.33;
-        res.rs = 0.93;
+        res.alpha = KCV(b, KC_A4);        // 0.6
+        res.ior = KCV(b, KC_IOR4);        // 1.33
+        res.rs = KCV(b, KC_RS4);          // 0.93
     }
     if (m == 3) {
-        res.alpha = 0.1;
-        res.ior = 1.50;
-        res.rs = 0.3;
+        res.alpha = KCV(b, KC_A3);        // 0.1
+        res.ior = KCV(b, KC_IOR3);        // 1.50
+        res.rs = KCV(b, KC_RS3);          // 0.3
     }
     return res;
 }
@@ -563,7 +571,7 @@ __device__ __forceinline__ double hue_to_rgb(double t1, double t2, double hue)
     if (hue > 1.0) hue -= 1.0;
     if (6.0 * hue < 1.0) return t1 + (t2 - t1) * 6.0 * hue;
     if (2.0 * hue < 1.0) return t2;
-    if (3.0 * hue < 2.0) return t1 + (t2 - t1) * ((2.0 / 3.0) - hue) * 6.0;
+    if (3.0 * hue < 2.0) return t1 + (t2 - t1) * (KCV(opq0(), KC_TWO_THIRDS) - hue) * 6.0;
     return t1;
 }
 __device__ __forceinline__ V3 hsl_roundtrip(V3 rgb)
@@ -588,7 +596,8 @@ __device__ __forceinline__ V3 hsl_roundtrip(V3 rgb)
     if (s == 0.0) return v3(l, l, l);
     const double t2 = (l < 0.5) ? (l * (1.0 + s)) : (l + s - l * s);
     const double t1 = 2.0 * l - t2;
-    return v3(hue_to_rgb(t1, t2, h + 1.0 / 3.0), hue_to_rgb(t1, t2, h), hue_to_rgb(t1, t2, h - 1.0 / 3.0));
+    const double third = KCV(opq0(), KC_THIRD);                 // 1.0 / 3.0
+    return v3(hue_to_rgb(t1, t2, h + third), hue_to_rgb(t1, t2, h), hue_to_rgb(t1, t2, h - third));
 }
 
 // ambient_occlusion, main.c:94-116: one cast, only distance/dst matters.
@@ -639,14 +648,21 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, 
         double t;
         int idx;
         const int kind = closest_hit<COUNT, BVH>(kp, o, d, t, idx, cnt);
-        V3 hp = v3(0, 0, 0), hn = v3(0, 0, 0);
-        Mat mat = Mat{v3(0, 0, 0), v3(0, 0, 0), 0.0, 0.0, 0.0, 0.0};
+        if (kind == HIT_NONE) {                          // miss: the path ends, main.c:236-238
+            if (chain) {                                 // albedo/normal of a missed chain ray: 0
+                acc_add(acc, 3, v3(0, 0, 0));            // (main.c:137-140 reads uninitialised
+                acc_add(acc, 6, v3(0, 0, 0));            //  fields; defined as 0)
+            }
+            break;
+        }
+        V3 hp, hn;
+        Mat mat;
         if (kind == HIT_SPHERE) {
             const SphGeo s = kp.sph[idx];
             hp = o + muls(d, t);                         // ray_at
             hn = normalize(hp - v3(s.cx, s.cy, s.cz));
             mat = load_mat(kp.sph_mat + idx);
-        } else if (kind == HIT_TRI) {
+        } else {
             if (COUNT) cnt.c[RT_CNT_TEX_HITS] += 1;
             const TriGeo g = kp.tri[idx];
             hp = o + muls(d, t);
@@ -656,20 +672,19 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, 
         if (chain) {
             // albedo/normal of this chain bounce are final unless it is an
             // alpha hole with bounces left (then the next bounce overwrites)
-            if (kind != HIT_NONE && mat.es > 0) {        // direct view of a light, main.c:154-160
+            if (mat.es > 0) {                            // direct view of a light, main.c:154-160
                 const V3 col = hsl_roundtrip(mat.emis);
                 acc_add(acc, 0, col);
                 acc_add(acc, 3, col);
                 acc_add(acc, 6, hn);
                 return;
             }
-            if (!(kind != HIT_NONE && mat.alpha < 0.0001) || i == kp.B - 1) {
+            if (!(mat.alpha < 0.0001) || i == kp.B - 1) {
                 acc_add(acc, 3, mat.diff);
                 acc_add(acc, 6, hn);
-                chain = kind != HIT_NONE && mat.alpha < 0.0001;   // stays on only for a last-bounce hole
+                chain = mat.alpha < 0.0001;              // stays on only for a last-bounce hole
             }
         }
-        if (kind == HIT_NONE) break;
         o = hp;
         const V3 diffuse_dir = normalize(hn + random_dir<COUNT>(st, cnt));
         const V3 reflected_dir = d - muls(hn, 2 * dot(d, hn));
