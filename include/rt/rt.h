@@ -182,6 +182,25 @@ int rt_count_async(const rt_device_scene* scene, const rt_params* params,
                    const rt_tiling* tiling, unsigned long long* d_counters,
                    void* hip_stream);
 
+/* ---- progressive rendering / checkpoint-resume ----------- */
+/* Adds samples [sample_offset, sample_offset + nbRayonParPixel) of every
+ * pixel of the tiling's local frame to the device accumulator d_sums (9
+ * doubles per local pixel: radiance, albedo, normal sums; local_rows*W
+ * entries, zero-filled by the caller before the first batch).  The stream is
+ * keyed by the global sample index, so with spp_chunks = 1 the sums after any
+ * sequence of batches covering samples 0..S-1 in order are bit-identical to
+ * one launch of S samples (fill_canva's fold continues across batches).  With
+ * spp_chunks = P > 1 a batch adds its P slice sums in slice order.  The sums
+ * are plain memory: copy them out to checkpoint, back in to resume.
+ * sample_offset + nbRayonParPixel must not exceed 2^32. */
+int rt_accumulate_async(const rt_device_scene* scene, const rt_params* params, long long sample_offset,
+                        const rt_tiling* tiling, double* d_sums, void* hip_stream);
+/* Writes the frame planes of d_sums for total_spp samples per pixel
+ * (write_color_canva with rapport = 1.0/total_spp, albedo/normal = sum /
+ * total_spp), main.c:275-279.  params supplies W and H. */
+int rt_resolve_async(const double* d_sums, const rt_params* params, int total_spp, const rt_tiling* tiling,
+                     const rt_frame* frame, void* hip_stream);
+
 /* ---- denoiser hook (denoiser.h:31-91, called at main.c:455) -------------- */
 /* denoiser()'s signature.  main.c runs it once on the finished frame when
  * useDenoiser is set; the OIDN library itself is not part of this one. */

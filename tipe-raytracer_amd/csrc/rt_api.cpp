@@ -477,6 +477,57 @@ int rt_render_async(const rt_device_scene* scene, const rt_params* params, const
     return launch_on_stream(kp, uni, (hipStream_t)hip_stream, false);
 }
 
+int rt_accumulate_async(const rt_device_scene* scene, const rt_params* params, long long sample_offset,
+                        const rt_tiling* tiling, double* d_sums, void* hip_stream)
+{
+    if (!scene) return fail(RT_EINVAL, "scene is NULL");
+    int rc;
+    if ((rc = validate_params(params)) || (rc = validate_tiling(tiling))) return rc;
+    if (!d_sums) return fail(RT_EINVAL, "d_sums is NULL");
+    if (sample_offset < 0 || sample_offset + params->nbRayonParPixel > (1ll << 32))
+        return fail(RT_EINVAL, "samples [%lld, %lld) exceed the 32-bit Philox sample word", sample_offset,
+                    sample_offset + params->nbRayonParPixel);
+    KParams kp;
+    double uni[U_COUNT];
+    make_kparams(scene, params, tiling, kp, uni);
+    kp.sums = d_sums;
+    kp.s_base = sample_offset;
+    if (kp.local_rows == 0 || kp.W == 0) return RT_OK;
+    DeviceGuard guard(scene->device);
+    return launch_on_stream(kp, uni, (hipStream_t)hip_stream, false);
+}
+
+int rt_resolve_async(const double* d_sums, const rt_params* params, int total_spp, const rt_tiling* tiling,
+                     const rt_frame* frame, void* hip_stream)
+{
+    int rc;
+    if ((rc = validate_tiling(tiling))) return rc;
+    if (!params || params->largeur_image < 1 || params->hauteur_image < 1) return fail(RT_EINVAL, "bad params");
+    if (!d_sums || !frame || !frame->canva) return fail(RT_EINVAL, "NULL buffer");
+    if (total_spp < 1) return fail(RT_EINVAL, "total_spp %d < 1", total_spp);
+    KParams kp;
+    std::memset(&kp, 0, sizeof kp);
+    kp.W = params->largeur_image;
+    kp.H = params->hauteur_image;
+    kp.S = total_spp;
+    kp.row_base = tiling->row_base;
+    kp.tile_rows = tiling->tile_rows;
+    kp.tile_first = tiling->tile_first;
+    kp.tile_step = tiling->tile_step;
+    kp.n_tiles = tiling->n_tiles;
+    kp.row_end = params->hauteur_image;
+    kp.local_rows = tiling->n_tiles * tiling->tile_rows;
+    kp.sums = (double*)d_sums;
+    kp.canva = (double*)frame->canva;
+    kp.albedo = (double*)frame->albedo;
+    kp.normal = (double*)frame->normal;
+    kp.radiance = (double*)frame->radiance;
+    if (kp.local_rows == 0) return RT_OK;
+    const int e = launch_resolve(kp, hip_stream);
+    if (e) return fail(RT_EDEVICE, "resolve launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
 int rt_count_async(const rt_device_scene* scene, const rt_params* params, const rt_tiling* tiling,
                    unsigned long long* d_counters, void* hip_stream)
 {

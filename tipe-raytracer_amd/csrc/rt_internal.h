@@ -83,6 +83,8 @@ struct KParams {
     double* normal;
     double* radiance;
     double* partial;         // chunks > 1: [chunks][band_rows*W][9]
+    double* sums;            // accumulate mode (rt_accumulate_async): [local_rows*W][9] running sums, or null
+    long long s_base;        // global index of this launch's first sample (Philox counter word 3)
     unsigned long long* counters;
 };
 
@@ -95,6 +97,7 @@ int launch_count(const KParams& kp, void* stream);
 int launch_assemble(const double* gathered, long long rank_stride, int world, int tile_rows,
                     int rows_per_rank, int W, int H, double* out, void* stream);
 int launch_selftest(int op, const double* d_in, double* d_out, int n, void* stream);
+int launch_resolve(const KParams& kp, void* stream);
 int launch_denoise_pack(long long npx, const double* canva, const double* albedo, const double* normal,
                         float* color3, float* albedo3, float* normal3, void* stream);
 

@@ -783,11 +783,15 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
         __shared__ double acc_lds[(BVH ? ACC_INC : ACC_SLOTS) * 256];
         __shared__ uint32_t rng_lds[4 * 256];
         double* acc = acc_lds + threadIdx.x;
+        const long long li = (long long)ly * kp.W + x;
+        // accumulate mode with one chunk continues the running sums in sample
+        // order (fill_canva's fold, carried across launches); otherwise 0
+        const bool carry = !COUNT && kp.sums && kp.chunks == 1;
 #pragma unroll
-        for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
+        for (int j = 0; j < 9; ++j) acc[j * 256] = carry ? kp.sums[li * 9 + j] : 0.0;
         for (int s = s0; s < s1; ++s) {
             Stream st;
-            st.start(pixel, (uint32_t)s, kp.key0, kp.key1, rng_lds + threadIdx.x);
+            st.start(pixel, (uint32_t)(kp.s_base + s), kp.key0, kp.key1, rng_lds + threadIdx.x);
             const double ju = -0.5 + 1.0 * unit31(st.next31());     // randomDouble(-0.5, 0.5)
             const double jv = -0.5 + 1.0 * unit31(st.next31());
             const double jx = -0.5 + 1.0 * unit31(st.next31());
@@ -813,11 +817,13 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
             }
         }
         if (!COUNT) {
-            const long long li = (long long)ly * kp.W + x;
             const V3 srad = v3(acc[0], acc[256], acc[512]);
             const V3 salb = v3(acc[768], acc[1024], acc[1280]);
             const V3 snrm = v3(acc[1536], acc[1792], acc[2048]);
-            if (kp.chunks == 1) {
+            if (carry) {
+#pragma unroll
+                for (int j = 0; j < 9; ++j) kp.sums[li * 9 + j] = acc[j * 256];
+            } else if (kp.chunks == 1) {
                 write_pixel(kp, li, srad, salb, snrm);
             } else {
                 double* p = kp.partial + ((long long)chunk * kp.band_rows * kp.W +
@@ -850,16 +856,28 @@ __global__ __launch_bounds__(256) void combine_kernel(const KParams kp)
         const int lt = ly / kp.tile_rows, yy = ly - lt * kp.tile_rows;
         const int g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + yy;
         if (g >= kp.row_end) continue;
-        const double* p = kp.partial + bi * 9;
         double a[9];
+        int c0 = 0;
+        if (kp.sums) {                                   // accumulate: running sums + slices in order
 #pragma unroll
-        for (int j = 0; j < 9; ++j) a[j] = p[j];
-        for (int c = 1; c < kp.chunks; ++c) {
+            for (int j = 0; j < 9; ++j) a[j] = kp.sums[li * 9 + j];
+        } else {
+            const double* p = kp.partial + bi * 9;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) a[j] = p[j];
+            c0 = 1;
+        }
+        for (int c = c0; c < kp.chunks; ++c) {
             const double* q = kp.partial + ((long long)c * npx + bi) * 9;
 #pragma unroll
             for (int j = 0; j < 9; ++j) a[j] = a[j] + q[j];
         }
-        write_pixel(kp, li, v3(a[0], a[1], a[2]), v3(a[3], a[4], a[5]), v3(a[6], a[7], a[8]));
+        if (kp.sums) {
+#pragma unroll
+            for (int j = 0; j < 9; ++j) kp.sums[li * 9 + j] = a[j];
+        } else {
+            write_pixel(kp, li, v3(a[0], a[1], a[2]), v3(a[3], a[4], a[5]), v3(a[6], a[7], a[8]));
+        }
     }
 }
 
@@ -961,6 +979,32 @@ int launch_denoise_pack(long long npx, const double* canva, const double* albedo
     hipLaunchKernelGGL(denoise_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, n, canva,
                        albedo ? albedo : nullptr, normal, color3, albedo ? albedo3 : nullptr,
                        normal ? normal3 : nullptr);
+    return (int)hipGetLastError();
+}
+
+// rt_resolve_async: running sums -> frame planes for kp.S total samples
+// (write_color_canva / divide_scalar, main.c:275-279).
+__global__ __launch_bounds__(256) void resolve_kernel(const KParams kp)
+{
+    const long long npx = (long long)kp.local_rows * kp.W;
+    for (long long li = (long long)blockIdx.x * blockDim.x + threadIdx.x; li < npx;
+         li += (long long)gridDim.x * blockDim.x) {
+        const int ly = (int)(li / kp.W);
+        const int lt = ly / kp.tile_rows, yy = ly - lt * kp.tile_rows;
+        const int g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + yy;
+        if (g >= kp.row_end) continue;
+        const double* a = kp.sums + li * 9;
+        write_pixel(kp, li, v3(a[0], a[1], a[2]), v3(a[3], a[4], a[5]), v3(a[6], a[7], a[8]));
+    }
+}
+
+int launch_resolve(const KParams& kp, void* stream)
+{
+    const long long npx = (long long)kp.local_rows * kp.W;
+    long long blocks = (npx + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(resolve_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, kp);
     return (int)hipGetLastError();
 }
 

@@ -58,6 +58,8 @@ def lib():
         L.rt_assemble_async.argtypes = [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_void_p, C.c_void_p]
         L.rt_selftest_math.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        L.rt_accumulate_async.argtypes = [C.c_void_p, P(Params), C.c_longlong, P(Tiling), C.c_void_p, C.c_void_p]
+        L.rt_resolve_async.argtypes = [C.c_void_p, P(Params), C.c_int, P(Tiling), P(Frame), C.c_void_p]
         L.rt_set_denoise_hook.argtypes = [DENOISE_FN]
         L.rt_get_denoise_hook.restype = C.c_void_p
         L.rt_denoise_pack.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6
@@ -70,7 +72,7 @@ def lib():
 EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error", "rt_version",
                     "rt_device_count", "rt_render_rows", "rt_fill_canva", "rt_scene_upload",
                     "rt_scene_release", "rt_render_async", "rt_assemble_async", "rt_count_async",
-                    "rt_selftest_math", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
+                    "rt_selftest_math", "rt_accumulate_async", "rt_resolve_async", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
                     "rt_denoise_unpack", "rt_denoise_pack_async"]
 
 # rt_denoise_fn (rt.h): denoiser()'s signature, denoiser.h:31
@@ -215,6 +217,19 @@ def render_async(dscene, params, tiling, canva_ptr, albedo_ptr=None, normal_ptr=
                  stream=None):
     fr = Frame(canva_ptr, albedo_ptr, normal_ptr, radiance_ptr)
     check(lib().rt_render_async(dscene.handle, C.byref(params), C.byref(tiling), C.byref(fr), stream))
+
+
+def accumulate_async(dscene, params, sample_offset, tiling, sums_ptr, stream=None):
+    """rt_accumulate_async: add samples [offset, offset + S) into d_sums."""
+    check(lib().rt_accumulate_async(dscene.handle, C.byref(params), sample_offset, C.byref(tiling), sums_ptr,
+                                    stream))
+
+
+def resolve_async(sums_ptr, params, total_spp, tiling, canva_ptr, albedo_ptr=None, normal_ptr=None,
+                  radiance_ptr=None, stream=None):
+    """rt_resolve_async: frame planes of the running sums for total_spp."""
+    fr = Frame(canva_ptr, albedo_ptr, normal_ptr, radiance_ptr)
+    check(lib().rt_resolve_async(sums_ptr, C.byref(params), total_spp, C.byref(tiling), C.byref(fr), stream))
 
 
 def count_async(dscene, params, tiling, counters_ptr, stream=None):
