@@ -225,7 +225,7 @@ def main():
                        "arith": "fp64, reference op order (bit-exact vs oracle)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP64_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / FP64_VECTOR_PEAK_TFLOPS, 4),
-                         "traffic": traffic, "kernel": "render_kernel<false, false>",
+                         "traffic": traffic, "kernel": "render_kernel<false, false, false>",
                          "kernel_ms": round(kernel_ms, 3), "flops_per_launch": flops,
                          "flops_per_sample": round(flops / launch_samples, 1),
                          "hbm": {"achieved_GBps": round(out_bytes / (kernel_ms * 1e-3) / 1e9, 4),

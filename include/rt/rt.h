@@ -52,6 +52,10 @@ typedef struct rt_scene {
     const rt_material* mat_list;       /* texel table, nbMaterials*th*tw, texture.h:175 */
     int tex_width, tex_height, nbMaterials;
     const int*         quelMatPourTri; /* per-triangle material, mesh.h:172        */
+    /* Equirect sky texels (create_mat_list of the sky PPM, main.c:374), used
+     * only with rt_params.sky_mode = RT_SKY_LAST_SPHERE; may be NULL. */
+    const rt_material* sky_mat_list;
+    int sky_width, sky_height;
 } rt_scene;
 
 /* ---- render parameters (main.c:293-347 constants, ThreadData fields) ---- */
@@ -77,7 +81,15 @@ typedef struct rt_params {
                                           samples run on P wavefronts          */
     unsigned long long seed;           /* Philox key                             */
     int accel;                         /* RT_ACCEL_*: triangle traversal          */
+    int sky_mode;                      /* RT_SKY_*                                */
 } rt_params;
+
+/* rt_params.sky_mode.  OFF is main.c as shipped (the sky branch of
+ * closest_hit is commented out, main.c:64-71).  LAST_SPHERE enables that
+ * branch: when the last sphere is the closest hit, its emissionColor becomes
+ * the sky texel sphere_uvmapping (texture.h:92-112) picks and its alpha 1. */
+#define RT_SKY_OFF 0
+#define RT_SKY_LAST_SPHERE 1
 
 /* rt_params.accel.  AUTO: scenes with more than 32 triangles get a BVH at
  * rt_scene_upload and closest-hit traverses it (the hit chosen is still the
@@ -227,7 +239,8 @@ int rt_denoise_pack_async(int W, int H, const rt_frame* frame, float* color3, fl
  * (synchronous, device 0).  op: 0 acos, 1 sinf, 2 cosf, 3 pow(x, y),
  * 4 sqrt, 5 x/y, 6 sqrtf, 7 philox word (in[0..3] = ctr, in[4..5] = key as
  * integers in doubles; returns 4 words per input), 8 normalize (3 doubles in,
- * 3 out, vec3.h:137-139).  Inputs are read as pairs (x, y) for binary ops. */
+ * 3 out, vec3.h:137-139), 9 atan2(y, x).  Inputs are read as pairs (x, y)
+ * for binary ops. */
 int rt_selftest_math(int op, const double* in, double* out, int n);
 
 #ifdef __cplusplus

@@ -205,4 +205,62 @@ static inline void pm_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+/* ---- atan2 (fdlibm scheme: s_atan.c reduction to 4 anchors + odd series,
+ * e_atan2.c quadrant logic), FMA-free as written here.  Used by the sky
+ * mapping (sphere_uvmapping, texture.h:92-112).  < 1 ulp; checked against
+ * libm in tests/test_oracle.py. */
+static const double PM_ATANHI[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
+                                    9.82793723247329054082e-01, 1.57079632679489655800e+00};
+static const double PM_ATANLO[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17,
+                                    1.39033110312309984516e-17, 6.12323399573676603587e-17};
+static const double PM_AT[11] = {3.33333333333329318027e-01, -1.99999999998764832476e-01,
+                                 1.42857142725034663711e-01, -1.11111104054623557880e-01,
+                                 9.09088713343650656196e-02, -7.69187620504482999495e-02,
+                                 6.66107313738753120669e-02, -5.83357013379057348645e-02,
+                                 4.97687799461593236017e-02, -3.65315727442169155270e-02,
+                                 1.62858201153657823623e-02};
+
+/* atan(a) for a >= 0, finite */
+static inline double pm_atan_pos(double a)
+{
+    int id;
+    double x = a;
+    if (a >= 0x1p66) return PM_ATANHI[3] + PM_ATANLO[3];
+    if (a < 0.4375) {
+        if (a < 0x1p-29) return a;
+        id = -1;
+    } else if (a < 1.1875) {
+        if (a < 0.6875) { id = 0; x = (2.0 * a - 1.0) / (2.0 + a); }
+        else            { id = 1; x = (a - 1.0) / (a + 1.0); }
+    } else if (a < 2.4375) { id = 2; x = (a - 1.5) / (1.0 + 1.5 * a); }
+    else                   { id = 3; x = -1.0 / a; }
+    double z = x * x;
+    double w = z * z;
+    double s1 = z * (PM_AT[0] + w * (PM_AT[2] + w * (PM_AT[4] + w * (PM_AT[6] + w * (PM_AT[8] + w * PM_AT[10])))));
+    double s2 = w * (PM_AT[1] + w * (PM_AT[3] + w * (PM_AT[5] + w * (PM_AT[7] + w * PM_AT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    return PM_ATANHI[id] - ((x * (s1 + s2) - PM_ATANLO[id]) - x);
+}
+
+static inline double pm_atan2(double y, double x)
+{
+    const double pi = 0x1.921fb54442d18p+1, pi_lo = 0x1.1a62633145c07p-53, pio2 = 0x1.921fb54442d18p+0;
+    if (x != x || y != y) return x + y;
+    if (y == 0.0) {
+        if (signbit(x)) return signbit(y) ? -pi : pi;      /* atan2(+-0, x<=-0) */
+        return y;                                           /* atan2(+-0, x>=+0) */
+    }
+    if (x == 0.0) return y > 0 ? pio2 : -pio2;
+    if (isinf(x)) {                                         /* C99 F.10.1.4 */
+        const double q = isinf(y) ? 0.5 * pio2 : 0.0;
+        const double r = x > 0 ? q : pi - q;
+        return y > 0 ? r : -r;
+    }
+    if (isinf(y)) return y > 0 ? pio2 : -pio2;
+    const double a = fabs(y / x);
+    double z = (fabs(y) > 0x1p60 * fabs(x)) ? pio2 : ((x < 0 && fabs(y) * 0x1p60 < fabs(x)) ? 0.0 : pm_atan_pos(a));
+    if (x > 0) return y > 0 ? z : -z;
+    return y > 0 ? pi - (z - pi_lo) : (z - pi_lo) - pi;
+}
+
 #endif /* PM_MATH_H */

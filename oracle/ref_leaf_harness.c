@@ -68,6 +68,20 @@ EXPORT void ref_tri_uvmapping(const triangle* tri, const ref_hit* hin, material*
     *out = tri_uvmapping(*tri, h, mat_list, tw, th, tri_index, quelMat);
 }
 
+EXPORT void ref_sphere_uvmapping(const point3* center, double radius, const point3* hitPoint, material* mat_list,
+                                 int w, int h, material* out)
+{
+    sphere s;
+    s.center = *center;
+    s.radius = radius;
+    HitInfo hi;
+    hi.didHit = true;
+    hi.dst = 1.0;
+    hi.hitPoint = *hitPoint;
+    hi.normal = vec3_init();
+    *out = sphere_uvmapping(s, hi, mat_list, w, h);
+}
+
 EXPORT void ref_refracted_vec(const vec3* v, const vec3* n, double n1, double n2, vec3* out)
 {
     *out = refracted_vec(*v, *n, n1, n2);

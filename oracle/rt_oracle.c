@@ -59,6 +59,7 @@ typedef struct ctx {
     int B, useAO;
     double AO;
     int rng, portable;
+    int sky;                 /* rt.h RT_SKY_LAST_SPHERE with a sky table */
     uint64_t seed;
     uint32_t pixel, sample, n;
     uint32_t block[4];
@@ -275,6 +276,26 @@ static rt_material tri_uvmapping(const rt_triangle* tri, const oracle_hit* h, co
     return res;
 }
 
+/* sphere_uvmapping, texture.h:92-112 (equirect sky texel).  The texel index
+ * is clamped into the table (the reference indexes unchecked). */
+static rt_material sphere_uvmapping(ctx* c, const rt_sphere* s, rt_vec3 hitPoint)
+{
+    const rt_scene* sc = c->sc;
+    const double PI = 3.1415926535897932385;               /* rtutility.h:14 */
+    const double inv = 1 / s->radius;                      /* divide(), vec3.h:105-107 */
+    rt_vec3 d = v3((hitPoint.e[0] - s->center.e[0]) * inv, (hitPoint.e[1] - s->center.e[1]) * inv,
+                   (hitPoint.e[2] - s->center.e[2]) * inv);
+    double theta = c->portable ? pm_acos(-d.e[1]) : acos(-d.e[1]);
+    double phi = (c->portable ? pm_atan2(-d.e[2], d.e[0]) : atan2(-d.e[2], d.e[0])) + PI;
+    double u = phi / (2 * PI), v = theta / PI;
+    int x = (int)(u * (double)(sc->sky_width));
+    int y = (int)(v * (double)(sc->sky_height));
+    long long index = (long long)y * sc->sky_width + x;
+    long long n = (long long)sc->sky_width * sc->sky_height;
+    index = index < 0 ? 0 : (index >= n ? n - 1 : index);
+    return sc->sky_mat_list[index];
+}
+
 /* closest_hit, main.c:52-92 (linear scan: spheres, then triangles) */
 static oracle_hit closest_hit(ctx* c, rt_ray r, int count_tex)
 {
@@ -290,6 +311,11 @@ static oracle_hit closest_hit(ctx* c, rt_ray r, int count_tex)
         if (h.didHit && h.dst < best.dst) {
             best = h;
             best.mat = s->mat;
+            if (c->sky && i == sc->nbSpheres - 1) {        /* main.c:64-71 (commented out there) */
+                rt_material sky_mat = sphere_uvmapping(c, s, h.hitPoint);
+                best.mat.emissionColor = sky_mat.diffuseColor;
+                best.mat.alpha = 1.0;
+            }
         }
     }
     int tri_won = 0;
@@ -532,6 +558,7 @@ static void init_ctx(ctx* c, const band* b)
     c->AO = b->AO;
     c->rng = b->p->rng;
     c->portable = b->portable;
+    c->sky = b->p->sky_mode == RT_SKY_LAST_SPHERE && b->sc->sky_mat_list && b->sc->nbSpheres > 0;
     c->seed = b->p->seed;
 }
 
@@ -750,6 +777,30 @@ double oracle_pm_acos(double x) { return pm_acos(x); }
 float oracle_pm_sinf(float x) { return pm_sinf(x); }
 float oracle_pm_cosf(float x) { return pm_cosf(x); }
 double oracle_pm_pow(double x, double y) { return pm_pow(x, y); }
+double oracle_pm_atan2(double y, double x) { return pm_atan2(y, x); }
+
+/* texel index sphere_uvmapping picks (test hook; portable: 0 libm, 1 pm_*) */
+long long oracle_sky_index(rt_vec3 center, double radius, rt_vec3 hitPoint, int w, int h, int portable)
+{
+    rt_material* mats = (rt_material*)calloc((size_t)w * h, sizeof(rt_material));
+    for (long long k = 0; k < (long long)w * h; ++k) mats[k].diffuseColor.e[0] = (double)k;
+    rt_scene sc;
+    memset(&sc, 0, sizeof sc);
+    sc.sky_mat_list = mats;
+    sc.sky_width = w;
+    sc.sky_height = h;
+    ctx c;
+    memset(&c, 0, sizeof c);
+    c.sc = &sc;
+    c.portable = portable;
+    rt_sphere s;
+    memset(&s, 0, sizeof s);
+    s.center = center;
+    s.radius = radius;
+    const long long k = (long long)sphere_uvmapping(&c, &s, hitPoint).diffuseColor.e[0];
+    free(mats);
+    return k;
+}
 void oracle_philox(const unsigned* ctr4, const unsigned* key2, unsigned* out4)
 {
     uint32_t c[4] = {ctr4[0], ctr4[1], ctr4[2], ctr4[3]}, k[2] = {key2[0], key2[1]}, o[4];

@@ -74,6 +74,8 @@ double oracle_pm_acos(double x);
 float  oracle_pm_sinf(float x);
 float  oracle_pm_cosf(float x);
 double oracle_pm_pow(double x, double y);
+double oracle_pm_atan2(double y, double x);
+long long oracle_sky_index(rt_vec3 center, double radius, rt_vec3 hitPoint, int w, int h, int portable);
 void   oracle_philox(const unsigned* ctr4, const unsigned* key2, unsigned* out4);
 /* Exhaustive scan: counts floats x in [lo, hi] (as float bit ranges) where
  * pm_sinf/pm_cosf differ from libm sinf/cosf.  Uses nthreads. */

@@ -214,6 +214,29 @@ def make_kat(lib, mesh):
         lib.ref_random_dir_no_norm(C.byref(o))
         dirs.append(v(o))
     kat["random_dir_no_norm_seed7"] = dirs
+    # sphere_uvmapping (texture.h:92-112, the sky mapping): texel k's diffuse
+    # red channel holds k, so the output names the index the reference picked.
+    # The table is padded so that the reference's unchecked index stays in
+    # memory; rows whose index falls outside w*h (its UB) are dropped.
+    srng = random.Random(2024)
+    rows = []
+    for w, h in ((8, 4), (64, 32), (7, 5)):
+        n = w * h
+        mats = (Material * (n + 4 * w + 8))()
+        for k in range(len(mats)):
+            mats[k].diffuseColor = Vec3(float(k), 0.0, 0.0)
+        for _ in range(120):
+            c = Vec3(*(srng.uniform(-3, 3) for _ in range(3)))
+            radius = srng.choice([0.5, 1.0, 500.0, srng.uniform(0.1, 50)])
+            dv = [srng.gauss(0, 1) for _ in range(3)]
+            nv = sum(x * x for x in dv) ** 0.5
+            p = Vec3(*(ci + radius * x / nv for ci, x in zip(c.tolist(), dv)))
+            out = Material()
+            lib.ref_sphere_uvmapping(C.byref(c), C.c_double(radius), C.byref(p), mats, w, h, C.byref(out))
+            k = int(out.diffuseColor.e[0])
+            if 0 <= k < n:
+                rows.append({"c": v(c), "r": hx(radius), "p": v(p), "w": w, "h": h, "index": k})
+    kat["sphere_uvmapping"] = rows
     return kat
 
 

@@ -19,14 +19,15 @@ def readme_camera_oracle():
 class SceneBundle:
     """Keeps the ctypes arrays alive next to the rt_scene that points at them."""
 
-    def __init__(self, spheres=None, mesh=None):
+    def __init__(self, spheres=None, mesh=None, sky=None):
         self.spheres = spheres
         self.mesh = mesh
+        self.sky = sky
         if mesh is not None:
             tris, qm, mats, tw, th, nm = mesh
-            self.scene = tipe_rt.make_scene(spheres, tris, qm, mats, tw, th, nm)
+            self.scene = tipe_rt.make_scene(spheres, tris, qm, mats, tw, th, nm, sky=sky)
         else:
-            self.scene = tipe_rt.make_scene(spheres)
+            self.scene = tipe_rt.make_scene(spheres, sky=sky)
 
 
 def cornell(extra=()):
@@ -37,17 +38,36 @@ def pyramid_scene(move=scenes.PYRAMID_MOVE):
     return SceneBundle(scenes.cornell_spheres(), scenes.moved(scenes.load_mesh_fixture("pyramide"), move))
 
 
+def sky_scene(w=16, h=8, seed=3):
+    """README spheres + an enclosing emissive sky sphere (the last sphere,
+    main.c:64-71) with a w x h equirect texel table of random colours."""
+    import ctypes as C
+    from tipe_rt.types import Sphere, Material, Vec3
+    base = scenes.cornell_spheres()
+    sph = (Sphere * (len(base) + 1))()
+    for k in range(len(base)):
+        sph[k] = base[k]
+    sph[len(base)].center = Vec3(0.0, 0.0, 0.0)
+    sph[len(base)].radius = 2000.0
+    sph[len(base)].mat = scenes.material((0.5, 0.5, 0.5), (1, 1, 1), 1.2, 0.0, 1.0, 1.0)
+    rng = np.random.default_rng(seed)
+    tex = (Material * (w * h))()
+    for k in range(w * h):
+        tex[k] = scenes.material(tuple(rng.uniform(0, 1, 3)), (0, 0, 0), 0.0, 0.0, 1.0, 0.0)
+    return SceneBundle(sph, None, sky=(tex, w, h))
+
+
 def tree_scene(move=scenes.TREE_MOVE):
     """C4: README spheres + 1tree_tri.obj (1320 tris, Kd-flat materials)."""
     return SceneBundle(scenes.cornell_spheres(), scenes.moved(scenes.load_tree_fixture(), move))
 
 
 def params(W, H, spp, bounces, use_ao=False, ao=2.5, rng=RT_RNG_PHILOX, seed=1010, compat=1, cam=None,
-           aperture=(0.0, 0.0), focus=3.0, chunks=1, accel=0):
+           aperture=(0.0, 0.0), focus=3.0, chunks=1, accel=0, sky_mode=0):
     if cam is None:
         cam = readme_camera_oracle()
     return tipe_rt.make_params(W, H, spp, bounces, cam, focus=focus, aperture=aperture, use_ao=use_ao, ao=ao,
-                               seed=seed, rng=rng, compat=compat, chunks=chunks, accel=accel)
+                               seed=seed, rng=rng, compat=compat, chunks=chunks, accel=accel, sky_mode=sky_mode)
 
 
 def oracle_render(bundle, p, row_hi=None, row_lo=0, nthreads=1, counters=False):

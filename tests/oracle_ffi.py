@@ -74,6 +74,10 @@ def oracle():
         lib.oracle_pm_cosf.restype = C.c_float
         lib.oracle_pm_pow.argtypes = [C.c_double, C.c_double]
         lib.oracle_pm_pow.restype = C.c_double
+        lib.oracle_pm_atan2.argtypes = [C.c_double, C.c_double]
+        lib.oracle_pm_atan2.restype = C.c_double
+        lib.oracle_sky_index.argtypes = [Vec3, C.c_double, Vec3, C.c_int, C.c_int, C.c_int]
+        lib.oracle_sky_index.restype = C.c_longlong
         lib.oracle_philox.argtypes = [P(C.c_uint), P(C.c_uint), P(C.c_uint)]
         ull = P(C.c_ulonglong)
         lib.oracle_scan_sincosf.argtypes = [C.c_float, C.c_float, C.c_int, ull, ull, ull]

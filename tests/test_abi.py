@@ -107,7 +107,7 @@ def test_validation_errors_without_device():
     p.rng = T.RT_RNG_PHILOX
     assert L.rt_render_rows(C.byref(sc), C.byref(p), 5, 0, buf, None, None) == T.RT_EINVAL
     assert L.rt_assemble_async(None, 0, 1, 1, 1, 1, 1, None, None) == T.RT_EINVAL
-    assert L.rt_selftest_math(9, buf, buf, 1) == T.RT_EINVAL
+    assert L.rt_selftest_math(10, buf, buf, 1) == T.RT_EINVAL
 
 
 def test_product_has_no_cpu_fallback(monkeypatch, tmp_path):
@@ -130,8 +130,8 @@ def test_kernel_resource_usage_builds_for_gfx950():
     out = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tipe-raytracer_amd"), "resource-usage"],
                          capture_output=True, text=True)
     txt = out.stdout + out.stderr
-    budgets = {"ILb0ELb0E": (128, 48),    # sphere scenes: 4 waves/SIMD
-               "ILb0ELb1E": (168, 32)}    # BVH scenes: 3 waves/SIMD (LDS stack)
+    budgets = {"ILb0ELb0ELb0E": (128, 48),    # sphere scenes: 4 waves/SIMD
+               "ILb0ELb1ELb0E": (168, 40)}    # BVH scenes: 3 waves/SIMD (LDS stack)
     for sym, (max_vgpr, max_spill) in budgets.items():
         m = re.search(r"render_kernel" + sym + r".*?VGPRs: (\d+).*?VGPRs Spill: (\d+)", txt, re.S)
         assert m, txt[-2000:]

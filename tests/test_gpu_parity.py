@@ -114,6 +114,28 @@ def test_device_normalize_fast_path_is_ieee():
     assert same.all(), v[~same.all(1)][:4]
 
 
+def test_device_atan2_matches_oracle():
+    o = oracle_ffi.oracle()
+    rng = np.random.default_rng(21)
+    n = 20000
+    yx = np.stack([np.concatenate([rng.uniform(-1, 1, n - 12), [0.0, -0.0, 0.0, -0.0, 1, -1, np.inf, 1, 1,
+                                                                  np.inf, -np.inf, 1e-300]]),
+                   np.concatenate([rng.uniform(-1, 1, n - 12), [1.0, 1.0, -1.0, -1.0, 0, 0, 1, np.inf, -np.inf,
+                                                                  np.inf, -np.inf, -1e300]])], 1)
+    got = tipe_rt.selftest_math(9, yx.ravel(), n)
+    want = np.array([o.oracle_pm_atan2(y, x) for y, x in yx])
+    assert (got.view(np.uint64) == want.view(np.uint64)).all()
+
+
+def test_sky_mode_last_sphere():
+    """main.c:64-71's commented-out sky branch (RT_SKY_LAST_SPHERE): the last
+    sphere shows sphere_uvmapping's texel as emission."""
+    bundle = helpers.sky_scene()
+    ref = check_parity(bundle, helpers.params(48, 36, 6, 5, sky_mode=1))
+    off = check_parity(bundle, helpers.params(48, 36, 6, 5, sky_mode=0))
+    assert not (ref["canva"] == off["canva"]).all()     # the sky changes the image
+
+
 def test_device_philox_matches_oracle():
     o = oracle_ffi.oracle()
     rng = np.random.default_rng(3)

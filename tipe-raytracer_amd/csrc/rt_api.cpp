@@ -78,6 +78,8 @@ int validate_scene(const rt_scene* sc)
                 return fail(RT_EINVAL, "quelMatPourTri[%d] = %d outside [0, %d)", i, sc->quelMatPourTri[i],
                             sc->nbMaterials);
     }
+    if (sc->sky_mat_list && (sc->sky_width < 1 || sc->sky_height < 1))
+        return fail(RT_EINVAL, "sky table %dx%d", sc->sky_width, sc->sky_height);
     return RT_OK;
 }
 
@@ -94,6 +96,8 @@ int validate_params(const rt_params* p)
                     "only the CPU oracle replays it");
     if (p->rng != RT_RNG_PHILOX) return fail(RT_EINVAL, "unknown rng %d", p->rng);
     if (p->accel != RT_ACCEL_AUTO && p->accel != RT_ACCEL_NONE) return fail(RT_EINVAL, "unknown accel %d", p->accel);
+    if (p->sky_mode != RT_SKY_OFF && p->sky_mode != RT_SKY_LAST_SPHERE)
+        return fail(RT_EINVAL, "unknown sky_mode %d", p->sky_mode);
     if ((unsigned long long)p->largeur_image * (unsigned long long)p->hauteur_image > 0xffffffffull)
         return fail(RT_EUNSUPPORTED, "pixel index exceeds the 32-bit Philox counter word");
     return RT_OK;
@@ -125,6 +129,9 @@ struct rt_device_scene {
     TriTex* tri_tex = nullptr;
     DevMat* texels = nullptr;
     BvhNode4* bvh = nullptr;         // 4-wide BVH; null: no BVH (few triangles)
+    DevMat* sky = nullptr;           // sky texels (scene->sky_mat_list), or null
+    double* sph_rinv = nullptr;      // 1/radius per sphere
+    int sky_w = 0, sky_h = 0;
     int* tri_orig = nullptr;         // leaf order -> caller's triangle index
     int bvh_nodes = 0, bvh_depth = 0;
     double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0;
@@ -149,6 +156,8 @@ void free_scene(rt_device_scene* s)
     (void)hipFree(s->tri_tex);
     (void)hipFree(s->texels);
     (void)hipFree(s->bvh);
+    (void)hipFree(s->sky);
+    (void)hipFree(s->sph_rinv);
     (void)hipFree(s->tri_orig);
     delete s;
 }
@@ -182,6 +191,12 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.tri_tex = sc->tri_tex;
     kp.texels = sc->texels;
     kp.tri_orig = sc->tri_orig;
+    kp.sph_rinv = sc->sph_rinv;
+    if (p->sky_mode == RT_SKY_LAST_SPHERE && sc->sky && sc->ns > 0) {
+        kp.sky = sc->sky;
+        kp.sky_w = sc->sky_w;
+        kp.sky_h = sc->sky_h;
+    }
     kp.ns = sc->ns;
     kp.ns_pad = sc->ns_pad;
     kp.nt = sc->nt;
@@ -359,11 +374,17 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     const int ns_pad = (scene->nbSpheres + 1) & ~1;
     std::vector<SphGeo> sph((size_t)ns_pad, SphGeo{0.0, 0.0, 0.0, -HUGE_VAL});
     std::vector<DevMat> sph_mat((size_t)scene->nbSpheres);
+    std::vector<double> sph_rinv((size_t)scene->nbSpheres);
     for (int i = 0; i < scene->nbSpheres; ++i) {
         const rt_sphere& s = scene->sphere_list[i];
         sph[i] = SphGeo{s.center.e[0], s.center.e[1], s.center.e[2], s.radius * s.radius};
         sph_mat[i] = to_dev(s.mat);
+        sph_rinv[i] = 1 / s.radius;                    // divide(v, t) = v * (1/t), vec3.h:105-107
     }
+    std::vector<DevMat> sky;
+    if (scene->sky_mat_list)
+        for (long long i = 0; i < (long long)scene->sky_width * scene->sky_height; ++i)
+            sky.push_back(to_dev(scene->sky_mat_list[i]));
     std::vector<TriGeo> tri((size_t)scene->nbTriangles);
     std::vector<TriTex> tex((size_t)scene->nbTriangles);
     for (int i = 0; i < scene->nbTriangles; ++i) {
@@ -441,6 +462,8 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->tw = scene->nbTriangles > 0 ? scene->tex_width : 1;
     ds->th = scene->nbTriangles > 0 ? scene->tex_height : 1;
     ds->n_texels = n_texels;
+    ds->sky_w = scene->sky_mat_list ? scene->sky_width : 0;
+    ds->sky_h = scene->sky_mat_list ? scene->sky_height : 0;
     ds->bvh_nodes = (int)bvh.nodes4.size();
     ds->bvh_depth = bvh.depth4;
     ds->s_rel = bvh.s_rel;
@@ -448,7 +471,8 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->r_scene = bvh.r_scene;
     if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
         (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels)) ||
-        (rc = upload(&ds->bvh, bvh.nodes4)) || (rc = upload(&ds->tri_orig, bvh.order))) {
+        (rc = upload(&ds->bvh, bvh.nodes4)) || (rc = upload(&ds->tri_orig, bvh.order)) ||
+        (rc = upload(&ds->sky, sky)) || (rc = upload(&ds->sph_rinv, sph_rinv))) {
         free_scene(ds);
         return rc;
     }
@@ -715,6 +739,7 @@ void* rt_fill_canva(void* arg)
     for (int i = 0; i < d->nbTriangles; ++i)
         if (d->quelMatPourTri && d->quelMatPourTri[i] + 1 > nmat) nmat = d->quelMatPourTri[i] + 1;
     rt_scene sc;
+    std::memset(&sc, 0, sizeof sc);
     sc.sphere_list = d->sphere_list;
     sc.nbSpheres = d->nbSpheres;
     sc.triangle_list = d->triangle_list;
@@ -724,6 +749,9 @@ void* rt_fill_canva(void* arg)
     sc.tex_height = d->tex_height;
     sc.nbMaterials = nmat;
     sc.quelMatPourTri = d->quelMatPourTri;
+    sc.sky_mat_list = d->sky_mat_list;        // carried like ThreadData does; sky_mode stays OFF (main.c)
+    sc.sky_width = d->sky_width;
+    sc.sky_height = d->sky_height;
     rt_params p;
     rt_params_init(&p);
     p.largeur_image = d->largeur_image;
@@ -743,7 +771,7 @@ void* rt_fill_canva(void* arg)
 
 int rt_selftest_math(int op, const double* in, double* out, int n)
 {
-    if (!in || !out || n < 0 || op < 0 || op > 8) return fail(RT_EINVAL, "bad selftest arguments");
+    if (!in || !out || n < 0 || op < 0 || op > 9) return fail(RT_EINVAL, "bad selftest arguments");
     if (n == 0) return RT_OK;
     int dev = 0;
     {
@@ -753,7 +781,7 @@ int rt_selftest_math(int op, const double* in, double* out, int n)
         dev = g_devices[0];
     }
     DeviceGuard guard(dev);
-    const size_t nin = (size_t)n * (op == 7 ? 6 : op == 8 ? 3 : (op == 3 || op == 5) ? 2 : 1);
+    const size_t nin = (size_t)n * (op == 7 ? 6 : op == 8 ? 3 : (op == 3 || op == 5 || op == 9) ? 2 : 1);
     const size_t nout = (size_t)n * (op == 7 ? 4 : op == 8 ? 3 : 1);
     double *d_in = nullptr, *d_out = nullptr;
     HIP_TRY(hipMalloc((void**)&d_in, nin * sizeof(double)));

@@ -41,6 +41,9 @@ enum : int {
     // literals: read at the point of use so they are never hoisted into
     // VGPRs (the compiler spilled them to scratch in every wave's prologue)
     KC_ES1, KC_A4, KC_IOR4, KC_RS4, KC_A3, KC_IOR3, KC_RS3, KC_THIRD, KC_TWO_THIRDS,
+    // atan2 (fdlibm, sky mapping)
+    KC_ATHI0, KC_ATHI1, KC_ATHI2, KC_ATHI3, KC_ATLO0, KC_ATLO1, KC_ATLO2, KC_ATLO3,
+    KC_AT0, KC_AT1, KC_AT2, KC_AT3, KC_AT4, KC_AT5, KC_AT6, KC_AT7, KC_AT8, KC_AT9, KC_AT10, KC_PI_LO53,
     KC_COUNT
 };
 
@@ -62,6 +65,11 @@ __constant__ const double kC[KC_COUNT] = {
     0x1.6c16c16c16c17p-10, 0x1.a01a01a01a01ap-13, 0x1.a01a01a01a01ap-16, 0x1.71de3a556c734p-19,
     0x1.27e4fb7789f5cp-22, 0x1.ae64567f544e4p-26, 0x1.1eed8eff8d898p-29, 0x1.6124613a86d09p-33,
     1.85, 0.6, 1.33, 0.93, 0.1, 1.50, 0.3, 1.0 / 3.0, 2.0 / 3.0,
+    4.63647609000806093515e-01, 7.85398163397448278999e-01, 9.82793723247329054082e-01, 1.57079632679489655800e+00,
+    2.26987774529616870924e-17, 3.06161699786838301793e-17, 1.39033110312309984516e-17, 6.12323399573676603587e-17,
+    3.33333333333329318027e-01, -1.99999999998764832476e-01, 1.42857142725034663711e-01, -1.11111104054623557880e-01,
+    9.09088713343650656196e-02, -7.69187620504482999495e-02, 6.66107313738753120669e-02, -5.83357013379057348645e-02,
+    4.97687799461593236017e-02, -3.65315727442169155270e-02, 1.62858201153657823623e-02, 0x1.1a62633145c07p-53,
 };
 
 // Scalar load of constant i (index laundered through b = opq0()).
@@ -230,6 +238,54 @@ __device__ __forceinline__ double pm_acos(double x)
         else res = (x - x) / (x - x);
     }
     return res;
+}
+
+// ---- atan2 (oracle/pm_math.h pm_atan2; sky mapping only) -------------------
+__device__ __forceinline__ double pm_atan_pos(int b, double a)
+{
+    int id;
+    double x = a;
+    if (a >= 0x1p66) return KCV(b, KC_ATHI3) + KCV(b, KC_ATLO3);
+    if (a < 0.4375) {
+        if (a < 0x1p-29) return a;
+        id = -1;
+    } else if (a < 1.1875) {
+        if (a < 0.6875) { id = 0; x = (2.0 * a - 1.0) / (2.0 + a); }
+        else            { id = 1; x = (a - 1.0) / (a + 1.0); }
+    } else if (a < 2.4375) { id = 2; x = (a - 1.5) / (1.0 + 1.5 * a); }
+    else                   { id = 3; x = -1.0 / a; }
+    const double z = x * x;
+    const double w = z * z;
+    const double s1 = z * (KCV(b, KC_AT0) + w * (KCV(b, KC_AT2) + w * (KCV(b, KC_AT4) + w * (KCV(b, KC_AT6) +
+                      w * (KCV(b, KC_AT8) + w * KCV(b, KC_AT10))))));
+    const double s2 = w * (KCV(b, KC_AT1) + w * (KCV(b, KC_AT3) + w * (KCV(b, KC_AT5) + w * (KCV(b, KC_AT7) +
+                      w * KCV(b, KC_AT9)))));
+    if (id < 0) return x - x * (s1 + s2);
+    return KCV(b, KC_ATHI0 + id) - ((x * (s1 + s2) - KCV(b, KC_ATLO0 + id)) - x);
+}
+
+__device__ __forceinline__ double pm_atan2(double y, double x)
+{
+    const int b = opq0();
+    const double pi = KCV(b, KC_PI), pi_lo = KCV(b, KC_PI_LO53), pio2 = KCV(b, KC_PIO2_HI);
+    const double inf = __longlong_as_double(0x7ff0000000000000ll);
+    if (x != x || y != y) return x + y;
+    if (y == 0.0) {
+        if (__signbit(x)) return __signbit(y) ? -pi : pi;
+        return y;
+    }
+    if (x == 0.0) return y > 0 ? pio2 : -pio2;
+    if (fabs(x) == inf) {
+        const double q = fabs(y) == inf ? 0.5 * pio2 : 0.0;
+        const double r = x > 0 ? q : pi - q;
+        return y > 0 ? r : -r;
+    }
+    if (fabs(y) == inf) return y > 0 ? pio2 : -pio2;
+    const double a = fabs(y / x);
+    const double z = (fabs(y) > 0x1p60 * fabs(x)) ? pio2
+                   : ((x < 0 && fabs(y) * 0x1p60 < fabs(x)) ? 0.0 : pm_atan_pos(b, a));
+    if (x > 0) return y > 0 ? z : -z;
+    return y > 0 ? pi - (z - pi_lo) : (z - pi_lo) - pi;
 }
 
 // ---- pow ---------------------------------------------------------------------

@@ -64,6 +64,9 @@ struct KParams {
     const double* uni;       // U_COUNT doubles
     const BvhNode4* bvh;     // 4-wide triangle BVH (rt_bvh.h), or null: brute-force scan
     const int* tri_orig;     // triangle k's index in the caller's list (null: k)
+    const DevMat* sky;       // sky texels when sky mode is on, else null
+    const double* sph_rinv;  // 1/radius per sphere (sphere_uvmapping's divide)
+    int sky_w, sky_h;
     double bvh_srel, bvh_sabs;   // distance-cull slack (rt_bvh.cpp)
     int ns, ns_pad, nt;
     int tw, th;

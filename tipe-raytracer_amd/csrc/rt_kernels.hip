@@ -515,6 +515,29 @@ __device__ __forceinline__ Mat tri_material(const KParams& kp, int k, const V3 P
     return res;
 }
 
+// Sky branch of closest_hit (main.c:64-71, commented out in the reference;
+// RT_SKY_LAST_SPHERE): emissionColor = sphere_uvmapping's texel (texture.h:
+// 92-112), alpha = 1.  The texel index is clamped into the table (the
+// reference indexes unchecked).
+__device__ __forceinline__ void sky_material(const KParams& kp, int idx, const SphGeo& s, V3 hp, Mat& mat)
+{
+    const double ri = kp.sph_rinv[idx];
+    const double dx = (hp.x - s.cx) * ri, dy = (hp.y - s.cy) * ri, dz = (hp.z - s.cz) * ri;
+    const int b = opq0();
+    const double PI = KCV(b, KC_PI);
+    const double theta = pm_acos(-dy);
+    const double phi = pm_atan2(-dz, dx) + PI;
+    const double u = phi / (2 * PI), v = theta / PI;
+    const int x = cvt_i32_x86(u * (double)kp.sky_w);
+    const int y = cvt_i32_x86(v * (double)kp.sky_h);
+    long long index = (long long)y * kp.sky_w + x;
+    const long long n = (long long)kp.sky_w * kp.sky_h;
+    index = index < 0 ? 0 : (index >= n ? n - 1 : index);
+    const DevMat* t = kp.sky + index;
+    mat.emis = v3(t->dr, t->dg, t->db);
+    mat.alpha = 1.0;
+}
+
 // random_dir_no_norm, rtutility.h:189-203 (float sinf/cosf of double args)
 template <bool COUNT>
 __device__ __forceinline__ V3 random_dir(Stream& st, Cnt& cnt)
@@ -633,7 +656,7 @@ __device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const
 // i == alpha_depth, i.e. along the primary chain of consecutive alpha holes,
 // and the next chain bounce always overwrites them; they are final when the
 // chain ends (first non-hole bounce, a miss, a light, or the last bounce).
-template <bool COUNT, bool BVH>
+template <bool COUNT, bool BVH, bool SKY>
 __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, Stream& st, double* acc, Cnt& cnt)
 {
     PathState<!BVH> ps{acc};
@@ -662,6 +685,7 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, 
             hp = o + muls(d, t);                         // ray_at
             hn = normalize(hp - v3(s.cx, s.cy, s.cz));
             mat = load_mat(kp.sph_mat + idx);
+            if (SKY && idx == kp.ns - 1) sky_material(kp, idx, s, hp, mat);
         } else {
             if (COUNT) cnt.c[RT_CNT_TEX_HITS] += 1;
             const TriGeo g = kp.tri[idx];
@@ -759,7 +783,7 @@ __device__ __forceinline__ void write_pixel(const KParams& kp, long long li, V3 
 }
 
 // fill_canva, main.c:245-284: thread = (pixel, chunk of its samples).
-template <bool COUNT, bool BVH>
+template <bool COUNT, bool BVH, bool SKY>
 __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIMD) void render_kernel(const KParams kp)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -810,7 +834,7 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
             const V3 dest = co + muls(dir, U[b + U_FOCUS]);
             const V3 no = co + v3(dx, dy, 0);
             const V3 rd = normalize(dest - no);
-            trace<COUNT, BVH>(kp, no, rd, U[b + U_AO], st, acc, cnt);
+            trace<COUNT, BVH, SKY>(kp, no, rd, U[b + U_AO], st, acc, cnt);
             if (COUNT) {
                 cnt.c[RT_CNT_SAMPLES] += 1;
                 cnt.c[RT_CNT_RNG_DRAWS] += st.n;
@@ -946,6 +970,7 @@ __global__ void selftest_kernel(int op, const double* __restrict__ in, double* _
         out[4 * i + 3] = p.w3;
         break;
     }
+    case 9: out[i] = pm_atan2(in[2 * i], in[2 * i + 1]); break;
     case 8: {                                   // normalize (fast lanes and generic lanes)
         const V3 v = normalize(v3(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
         out[3 * i + 0] = v.x;
@@ -1013,12 +1038,23 @@ static dim3 grid_for(const KParams& kp)
     return dim3((unsigned)((kp.W + 15) / 16), (unsigned)((kp.band_rows + 15) / 16), (unsigned)kp.chunks);
 }
 
+// Kernel instantiation per scene features: BVH traversal and the sky branch
+// are compiled only into the variants that use them, so a sphere-only scene
+// runs a kernel without their registers.
+template <bool COUNT>
+static void launch_variant(const KParams& kp, void* stream)
+{
+    const dim3 g = grid_for(kp);
+    const hipStream_t st = (hipStream_t)stream;
+    if (kp.bvh && kp.sky) hipLaunchKernelGGL((render_kernel<COUNT, true, true>), g, dim3(256), 0, st, kp);
+    else if (kp.bvh) hipLaunchKernelGGL((render_kernel<COUNT, true, false>), g, dim3(256), 0, st, kp);
+    else if (kp.sky) hipLaunchKernelGGL((render_kernel<COUNT, false, true>), g, dim3(256), 0, st, kp);
+    else hipLaunchKernelGGL((render_kernel<COUNT, false, false>), g, dim3(256), 0, st, kp);
+}
+
 int launch_render(const KParams& kp, void* stream)
 {
-    if (kp.bvh)
-        hipLaunchKernelGGL((render_kernel<false, true>), grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
-    else
-        hipLaunchKernelGGL((render_kernel<false, false>), grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
+    launch_variant<false>(kp, stream);
     if (kp.chunks > 1) {
         const long long npx = (long long)kp.band_rows * kp.W;
         long long blocks = (npx + 255) / 256;
@@ -1030,10 +1066,7 @@ int launch_render(const KParams& kp, void* stream)
 
 int launch_count(const KParams& kp, void* stream)
 {
-    if (kp.bvh)
-        hipLaunchKernelGGL((render_kernel<true, true>), grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
-    else
-        hipLaunchKernelGGL((render_kernel<true, false>), grid_for(kp), dim3(256), 0, (hipStream_t)stream, kp);
+    launch_variant<true>(kp, stream);
     return (int)hipGetLastError();
 }
 

@@ -134,9 +134,14 @@ def init_camera(origin, target, up, vfov, ratio):
 
 
 def make_scene(spheres=None, triangles=None, quel_mat=None, mat_list=None, tex_width=0, tex_height=0,
-               n_materials=0):
+               n_materials=0, sky=None):
+    """rt_scene over ctypes arrays; sky = (texels, width, height) or None."""
     sc = Scene()
     keep = []
+    if sky is not None:
+        sc.sky_mat_list = C.cast(sky[0], C.POINTER(Material))
+        sc.sky_width, sc.sky_height = sky[1], sky[2]
+        keep.append(sky[0])
     if spheres is not None and len(spheres):
         sc.sphere_list = C.cast(spheres, C.POINTER(Sphere))
         sc.nbSpheres = len(spheres)
@@ -153,7 +158,7 @@ def make_scene(spheres=None, triangles=None, quel_mat=None, mat_list=None, tex_w
 
 
 def make_params(W, H, spp, bounces, cam, focus=3.0, aperture=(0.0, 0.0), use_ao=False, ao=2.5,
-                seed=1010, rng=RT_RNG_PHILOX, compat=1, chunks=1, accel=0):
+                seed=1010, rng=RT_RNG_PHILOX, compat=1, chunks=1, accel=0, sky_mode=0):
     p = Params()
     p.largeur_image, p.hauteur_image = W, H
     p.nbRayonParPixel, p.nbRebondMax = spp, bounces
@@ -165,6 +170,7 @@ def make_params(W, H, spp, bounces, cam, focus=3.0, aperture=(0.0, 0.0), use_ao=
     p.rng, p.seed = rng, seed
     p.spp_chunks = chunks
     p.accel = accel
+    p.sky_mode = sky_mode
     return p
 
 

@@ -13,6 +13,7 @@ COUNTER_NAMES = ["samples", "casts", "sphere_tests", "sphere_disc", "tri_tests",
                  "shade", "tex_hits", "refract", "rng_draws", "exact_rescans",
                  "bvh_nodes", "bvh_tri_tests"]
 RT_ACCEL_AUTO, RT_ACCEL_NONE = 0, 1
+RT_SKY_OFF, RT_SKY_LAST_SPHERE = 0, 1
 
 
 class Vec3(C.Structure):
@@ -81,7 +82,8 @@ class Scene(C.Structure):
                 ("triangle_list", C.POINTER(Triangle)), ("nbTriangles", C.c_int),
                 ("mat_list", C.POINTER(Material)),
                 ("tex_width", C.c_int), ("tex_height", C.c_int), ("nbMaterials", C.c_int),
-                ("quelMatPourTri", C.POINTER(C.c_int))]
+                ("quelMatPourTri", C.POINTER(C.c_int)),
+                ("sky_mat_list", C.POINTER(Material)), ("sky_width", C.c_int), ("sky_height", C.c_int)]
 
 
 class Params(C.Structure):
@@ -92,7 +94,8 @@ class Params(C.Structure):
                 ("ouverture_x", C.c_double), ("ouverture_y", C.c_double),
                 ("AO_intensity", C.c_double), ("useAO", C.c_int),
                 ("compat_int_truncation", C.c_int), ("rng", C.c_int),
-                ("spp_chunks", C.c_int), ("seed", C.c_ulonglong), ("accel", C.c_int)]
+                ("spp_chunks", C.c_int), ("seed", C.c_ulonglong), ("accel", C.c_int),
+                ("sky_mode", C.c_int)]
 
 
 class Tiling(C.Structure):

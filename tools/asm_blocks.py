@@ -1,6 +1,6 @@
 """Per-basic-block instruction census of a kernel in rt_kernels.s (make -C
 tipe-raytracer_amd asm).  Usage: [KERNEL=sym] python tools/asm_blocks.py [min_valu] [asm]
-Default kernel: render_kernel<false, false> (the sphere-scene render)."""
+Default kernel: render_kernel<false, false, false> (the sphere-scene render)."""
 import collections
 import os
 import re
@@ -8,7 +8,7 @@ import sys
 
 path = sys.argv[2] if len(sys.argv) > 2 else "tipe-raytracer_amd/rt_kernels.s"
 s = open(path).read()
-KERNEL = os.environ.get("KERNEL", "_ZN2rt13render_kernelILb0ELb0EEEvNS_7KParamsE")
+KERNEL = os.environ.get("KERNEL", "_ZN2rt13render_kernelILb0ELb0ELb0EEEvNS_7KParamsE")
 start = s.index(KERNEL + ":")
 body = s[start:s.index("s_endpgm", start)].splitlines()
 blocks, cur = [], ["entry", [], ""]
