@@ -253,10 +253,11 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             const double disc = b * b - four_a * c;
             if (disc > 0) {
                 if (COUNT) cnt.c[RT_CNT_SPHERE_DISC] += 1;
-                if (!(disc >= 0x1p-900 && disc <= 0x1p900)) {
-                    amb = true;
-                    continue;
-                }
+#ifndef RT_CAND_BRANCHY
+                // Straight-line: both roots, the acceptance logic as masks and
+                // the interval update as selects (no phi copies, no exec
+                // juggling).  Out-of-range disc (rsq invalid) -> ambiguous.
+                const bool inr = disc >= 0x1p-900 && disc <= 0x1p900;
                 // sa ~ sqrt(disc): v_rsq_f64 + one Newton step folded into
                 // sa = t + t*e/2, t = disc*r0, e = 1 - t*r0 (fma).
                 const double r0 = __builtin_amdgcn_rsq(disc);
@@ -264,6 +265,27 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
                 const double sa = fma(tt * 0.5, fma(-tt, r0, 1.0), tt);
                 // one margin for both roots: (|b| + sa)/(2a) * 2^-38 bounds
                 // sa*inv2a*2^-39.7 + |q|*2^-50
+                const double M = (fabs(b) + sa) * inv2a_m;
+                const double q1 = (-b - sa) * inv2a, q2 = (sa - b) * inv2a;   // t1, t2
+                const bool c1 = q1 - M >= 0.0001, a1 = q1 + M >= 0.0001;      // surely / maybe >= 1e-4
+                const bool c2 = q2 - M >= 0.0001, a2 = q2 + M >= 0.0001;
+                const bool use2 = !a1 && c2;
+                const bool cand = inr && (c1 || use2);
+                const double q = c1 ? q1 : q2;
+                const double lo = q - M, hi = q + M;
+                const bool closer = cand && hi < blo;
+                amb = amb || !inr || (a1 && !c1) || (!a1 && !c2 && a2) || (cand && !closer && !(lo >= bhi));
+                blo = closer ? lo : blo;
+                bhi = closer ? hi : bhi;
+                bk = closer ? k + h : bk;
+#else
+                if (!(disc >= 0x1p-900 && disc <= 0x1p900)) {
+                    amb = true;
+                    continue;
+                }
+                const double r0 = __builtin_amdgcn_rsq(disc);
+                const double tt = disc * r0;
+                const double sa = fma(tt * 0.5, fma(-tt, r0, 1.0), tt);
                 const double M = (fabs(b) + sa) * inv2a_m;
                 double q = (-b - sa) * inv2a;              // near root t1
                 if (!(q - M >= 0.0001)) {
@@ -278,11 +300,12 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
                     }
                 }
                 const double lo = q - M, hi = q + M;
-                const bool closer = hi < blo;             // selects, not branches (fewer phi copies)
+                const bool closer = hi < blo;
                 amb = amb || (!closer && !(lo >= bhi));
                 blo = closer ? lo : blo;
                 bhi = closer ? hi : bhi;
                 bk = closer ? k + h : bk;
+#endif
             }
         }
     }
