@@ -42,8 +42,12 @@ out = {"kernel": render["Name"], "calls": int(render["Calls"]), "avg_ms": dur_ns
        "wait_inst_any_frac": s["SQ_WAIT_INST_ANY"] / s["SQ_WAVE_CYCLES"] if s["SQ_WAVE_CYCLES"] else None,
        "valu_lane_utilization": (fl["SQ_THREAD_CYCLES_VALU"] / (fl["SQ_ACTIVE_INST_VALU"] * 64)
                                  if fl["SQ_THREAD_CYCLES_VALU"] and fl["SQ_ACTIVE_INST_VALU"] else None),
-       "hw_fp64_tflops": (fl["SQ_INSTS_VALU_FLOPS_FP64"] / (dur_ns * 1e-9) / 1e12
-                          if fl["SQ_INSTS_VALU_FLOPS_FP64"] else None),
+       # SQ_INSTS_VALU_FLOPS_FP64 counts per wave instruction (FMA = 2): it equals
+       # ADD_F64 + MUL_F64 + 2*FMA_F64 + TRANS_F64 exactly, so lane FLOPs are x64,
+       # scaled by the measured lane utilization.
+       "hw_fp64_tflops": (fl["SQ_INSTS_VALU_FLOPS_FP64"] * 64 * (fl["SQ_THREAD_CYCLES_VALU"] / (fl["SQ_ACTIVE_INST_VALU"] * 64))
+                          / (dur_ns * 1e-9) / 1e12
+                          if fl["SQ_INSTS_VALU_FLOPS_FP64"] and fl["SQ_ACTIVE_INST_VALU"] else None),
        "note": "FETCH_SIZE doubled (gfx950 reports half of wide-load bytes, MI355X_MICROARCH.md HBM); "
                "units KiB; per render_kernel<false, false, false> launch; PMC runs are separate rocprofv3 passes"}
 json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
@@ -58,6 +62,6 @@ for f in ["bench.json", "host_path.json", "pytest_gpu.log", "demo.log"]:
     if os.path.exists(p):
         os.system("cp %s %s" % (p, os.path.join(dst, f)))
 json.dump({"render_kernel_hbm_bytes_per_launch": hbm, "source": dst + "/summary.json",
-           "workload": "C2 1200x900 1000spp 6 bounces, spp_chunks 8"},
+           "workload": "C2 1200x900 1000spp 6 bounces, spp_chunks 32"},
           open(os.path.join("profiles", "pmc_traffic.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
