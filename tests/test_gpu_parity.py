@@ -257,6 +257,40 @@ def test_bvh_tie_break_on_duplicate_triangles():
     check_parity(bundle, helpers.params(24, 18, 2, 6, accel=1))
 
 
+def adversarial_sphere_scene():
+    """Sphere pairs the candidate pass cannot separate (spheres_closest):
+    an exact duplicate (equal t: the reference keeps the first), a sphere
+    1e-12 larger than its neighbour, spheres touching each other and the
+    floor, a tiny sphere and a huge far one.  Each must fall back to the
+    exact scan or be resolved exactly."""
+    m = tipe_rt.scenes.material
+    extra = [
+        ((0.3, 0.2, -2.5), 0.3, m((1, 0, 0))),
+        ((0.3, 0.2, -2.5), 0.3, m((0, 1, 0), refl=0.5)),                 # duplicate: first wins
+        ((-0.4, 0.1, -2.0), 0.25, m((0, 0, 1))),
+        ((-0.4, 0.1, -2.0), 0.25 + 1e-12, m((1, 1, 0))),                  # 1e-12 apart
+        ((0.0, -0.5, -1.8), 0.5, m((0.9, 0.9, 0.9), refl=0.9)),          # touches the floor (y = -1)
+        ((0.5, -0.5, -1.8), 0.5, m((0.2, 0.8, 0.5))),        # touches the previous one
+        ((0.05, 0.3, -1.2), 1e-4, m((1, 1, 1), (1, 1, 1), 3.0)),         # tiny emitter
+        ((0.0, 0.0, -2e4), 1e4, m((0.5, 0.5, 0.5))),                     # huge, far
+    ]
+    return helpers.cornell(extra)
+
+
+def test_sphere_candidate_pass_adversarial():
+    import torch
+    bundle = adversarial_sphere_scene()
+    check_parity(bundle, helpers.params(48, 36, 8, 6))
+    check_parity(bundle, helpers.params(32, 24, 4, 6, use_ao=True, ao=2.5, compat=0))
+    p = helpers.params(48, 36, 4, 6)
+    ds = tipe_rt.DeviceScene(bundle.scene, 0)
+    d_cnt = torch.zeros(tipe_rt.RT_NCOUNTERS, dtype=torch.int64, device="cuda:0")
+    tipe_rt.count_async(ds, p, tipe_rt.band_tiling(0, 35), d_cnt.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ds.close()
+    assert d_cnt[tipe_rt.types.RT_CNT_EXACT_RESCANS].item() > 0      # the fallback scan ran
+
+
 @pytest.mark.parametrize("W,H", [(1, 1), (1, 5), (5, 1), (2, 2), (17, 3)])
 def test_degenerate_frames(W, H):
     """largeur_image or hauteur_image of 1 makes main.c:265 divide by zero

@@ -124,6 +124,8 @@ struct rt_device_scene {
     int ns = 0, ns_pad = 0, nt = 0, tw = 1, th = 1;
     long long n_texels = 0;
     SphGeo* sph = nullptr;
+    SphCand* sph_cand = nullptr;
+    double cand_lmax = HUGE_VAL;
     DevMat* sph_mat = nullptr;
     TriGeo* tri = nullptr;
     TriTex* tri_tex = nullptr;
@@ -151,6 +153,7 @@ void free_scene(rt_device_scene* s)
     if (!s) return;
     DeviceGuard g(s->device);
     (void)hipFree(s->sph);
+    (void)hipFree(s->sph_cand);
     (void)hipFree(s->sph_mat);
     (void)hipFree(s->tri);
     (void)hipFree(s->tri_tex);
@@ -186,6 +189,8 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
 {
     std::memset(&kp, 0, sizeof kp);
     kp.sph = sc->sph;
+    kp.sph_cand = sc->sph_cand;
+    kp.cand_lmax = sc->cand_lmax;
     kp.sph_mat = sc->sph_mat;
     kp.tri = sc->tri;
     kp.tri_tex = sc->tri_tex;
@@ -373,14 +378,26 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     // the discriminant -inf): the kernel reads them two per s_load_dwordx16.
     const int ns_pad = (scene->nbSpheres + 1) & ~1;
     std::vector<SphGeo> sph((size_t)ns_pad, SphGeo{0.0, 0.0, 0.0, -HUGE_VAL});
+    std::vector<SphCand> cand((size_t)ns_pad, SphCand{0.0, 0.0, 0.0, HUGE_VAL});
     std::vector<DevMat> sph_mat((size_t)scene->nbSpheres);
     std::vector<double> sph_rinv((size_t)scene->nbSpheres);
+    // Candidate-pass bound L >= |C_k| + R_k for every sphere (rounded up, at
+    // least 2^-20); a non-finite sphere makes it +inf, which turns the
+    // candidate pass into the exact scan (rt_kernels.hip spheres_closest).
+    long double lmax = 0x1p-20L;
     for (int i = 0; i < scene->nbSpheres; ++i) {
         const rt_sphere& s = scene->sphere_list[i];
-        sph[i] = SphGeo{s.center.e[0], s.center.e[1], s.center.e[2], s.radius * s.radius};
+        const double r2 = s.radius * s.radius;
+        sph[i] = SphGeo{s.center.e[0], s.center.e[1], s.center.e[2], r2};
+        const long double cx = s.center.e[0], cy = s.center.e[1], cz = s.center.e[2];
+        const long double c2 = cx * cx + cy * cy + cz * cz;
+        cand[i] = SphCand{s.center.e[0], s.center.e[1], s.center.e[2], (double)(c2 - (long double)r2)};
+        const long double L = (std::sqrt(c2) + std::fabs((long double)s.radius)) * (1.0L + 0x1p-40L);
+        lmax = std::isfinite((double)L) && !std::isnan((double)cand[i].k) ? std::max(lmax, L) : (long double)HUGE_VAL;
         sph_mat[i] = to_dev(s.mat);
         sph_rinv[i] = 1 / s.radius;                    // divide(v, t) = v * (1/t), vec3.h:105-107
     }
+    const double cand_lmax = std::isfinite((double)lmax) ? std::nextafter((double)lmax, HUGE_VAL) : HUGE_VAL;
     std::vector<DevMat> sky;
     if (scene->sky_mat_list)
         for (long long i = 0; i < (long long)scene->sky_width * scene->sky_height; ++i)
@@ -458,6 +475,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->device = device;
     ds->ns = scene->nbSpheres;
     ds->ns_pad = ns_pad;
+    ds->cand_lmax = cand_lmax;
     ds->nt = scene->nbTriangles;
     ds->tw = scene->nbTriangles > 0 ? scene->tex_width : 1;
     ds->th = scene->nbTriangles > 0 ? scene->tex_height : 1;
@@ -469,7 +487,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->s_rel = bvh.s_rel;
     ds->s_abs = bvh.s_abs;
     ds->r_scene = bvh.r_scene;
-    if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
+    if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_cand, cand)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
         (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels)) ||
         (rc = upload(&ds->bvh, bvh.nodes4)) || (rc = upload(&ds->tri_orig, bvh.order)) ||
         (rc = upload(&ds->sky, sky)) || (rc = upload(&ds->sph_rinv, sph_rinv))) {

@@ -2,10 +2,12 @@
 // the C-ABI (rt_api.cpp) and the kernels (rt_kernels.hip).
 //
 // HBM layout of one uploaded scene (DESIGN.md "Data layout"):
-//   SphGeo  [ns_pad] 32 B  center, radius^2 — scanned wave-uniformly through
-//                          the scalar unit, two records per s_load_dwordx16;
-//                          padded to an even count with never-hit records
-//                          (radius^2 = -inf => discriminant = -inf)
+//   SphCand [ns_pad] 32 B  center, |C|^2 - radius^2 — the candidate pass,
+//                          scanned wave-uniformly through the scalar unit,
+//                          two records per s_load_dwordx16; padded to an even
+//                          count with never-hit records (k = +inf)
+//   SphGeo  [ns_pad] 32 B  center, radius^2 — the exact reference test
+//                          (winner, fallback scan; r2 = -inf padding)
 //   DevMat  [ns]     80 B  sphere material — gathered for the winner only
 //   TriGeo  [nt]     96 B  A, B-A, C-A, N  — scanned wave-uniformly
 //   TriTex  [nt]    104 B  B, C, uvA/B/C, material — winner only
@@ -24,6 +26,10 @@ namespace rt {
 struct BvhNode4;                                      // rt_bvh.h
 
 struct SphGeo { double cx, cy, cz, r2; };            // r2 = radius*radius (sphere.h:22)
+// Candidate-pass record (rt_kernels.hip spheres_closest): center and
+// k = |C|^2 - r2 (host, long double), so c*a = a*|o|^2 - 2a*o.C + a*k is an
+// FMA chain; padding records have k = +inf (never hit).
+struct SphCand { double cx, cy, cz, k; };
 struct DevMat {                                       // == material, hitinfo.h:6-13
     double dr, dg, db;       // diffuseColor
     double er, eg, eb;       // emissionColor
@@ -42,6 +48,7 @@ struct TriTex {                                       // what tri_uvmapping read
     int pad;
 };
 static_assert(sizeof(SphGeo) == 32, "SphGeo");
+static_assert(sizeof(SphCand) == 32, "SphCand");
 static_assert(sizeof(DevMat) == 80, "DevMat");
 static_assert(sizeof(TriGeo) == 96, "TriGeo");
 static_assert(sizeof(TriTex) == 104, "TriTex");
@@ -57,6 +64,8 @@ enum : int {
 struct KParams {
     // scene
     const SphGeo* sph;
+    const SphCand* sph_cand; // candidate-pass records [ns_pad]
+    double cand_lmax;        // >= max_k |C_k| + R_k (+inf: candidate pass off, exact scans)
     const DevMat* sph_mat;
     const TriGeo* tri;
     const TriTex* tri_tex;

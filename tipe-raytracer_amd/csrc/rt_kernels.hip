@@ -46,6 +46,17 @@
 #include "rt_bvh.h"
 #include "rt_device_math.h"
 
+// Candidate-pass grazing threshold T1 = RT_CAND_T1 * Hs^2 and half-width
+// M = RT_CAND_M * Hs (spheres_closest); M must exceed 2^-47.2 / sqrt(RT_CAND_T1)
+// by a wide factor (static_assert below).
+#ifndef RT_CAND_T1
+#define RT_CAND_T1 0x1p-36
+#endif
+#ifndef RT_CAND_M
+#define RT_CAND_M 0x1p-26
+#endif
+static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x1p-20,
+              "candidate half-width M must be >= 8 x the sqrt error bound 2^-47.2/sqrt(T1)");
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -221,94 +232,110 @@ __device__ __forceinline__ bool sphere_exact(double cx, double cy, double cz, do
     return false;
 }
 
-// Closest sphere (main.c:59-78).  Candidate pass with error intervals, then
-// the exact test for the winner; exact scan on any ambiguity.
-//
-// Interval bound (DESIGN.md "Exact closest hit"): sa, one Newton step from
-// v_rsq_f64, has |sa/sqrt(disc) - 1| <= 2^-45 (measured 2^-47.7 over 1e9
-// inputs; v_rsq_f64 <= 2^-24.2), so with q = RN(n_a*inv2a) the exact root t
-// satisfies |t - q| <= sa*inv2a*2^-39.7 + |q|*2^-50 < (|b| + sa)*inv2a*2^-39
-// (|q| <= (|b| + sa)*inv2a); the margin used, M = (|b| + sa)*inv2a*2^-38,
-// also absorbs the rounding of M and of the interval end points.
-template <bool COUNT>
-__device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, const V3 d, double two_a,
-                                               double four_a, double inv2a, bool fast, double rc2a,
-                                               double& t_best, Cnt& cnt)
+// The reference's discriminant sign (sphere.h:24-25): COUNT statistics only.
+__device__ __forceinline__ bool disc_positive(const SphGeo& s, const V3 o, const V3 d, double four_a)
+{
+    const double ocx = o.x - s.cx, ocy = o.y - s.cy, ocz = o.z - s.cz;
+    const double b = 2.0 * (ocx * d.x + ocy * d.y + ocz * d.z);
+    const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - s.r2;
+    return b * b - four_a * c > 0;
+}
+
+// Exact reference scan over every sphere (main.c:59-78 with hit_sphere).
+__device__ __forceinline__ int spheres_exact_scan(const KParams& kp, const V3 o, const V3 d, double two_a,
+                                                  double four_a, bool fast, double rc2a, double& t_best)
 {
     const cdptr sg = (cdptr)kp.sph;
+    double t = dinf();
+    int win = -1;
+    for (int k = 0; k < kp.ns_pad; ++k) {
+        double tk;
+        if (sphere_exact(sg[4 * k], sg[4 * k + 1], sg[4 * k + 2], sg[4 * k + 3], o, d, two_a, four_a, fast, rc2a,
+                         tk) &&
+            tk < t) {
+            t = tk;
+            win = k;
+        }
+    }
+    t_best = t;
+    return win;
+}
+
+// Closest sphere (main.c:59-78): an FMA candidate pass with rigorous error
+// intervals picks the winner, whose exact reference test then runs alone;
+// any ambiguity reruns the exact scan for that ray (DESIGN.md "Exact closest
+// hit").  Half-b form: h = (o-C).d, D = h^2 - a*c, roots n1,2 = -h -/+ sqrt(D)
+// with t = n/a (the reference's t1,2 = (-b -/+ sqrt(disc))/(2a) scale
+// exactly: b = 2h, disc = 4D).  Intervals are kept in n = a*t units, one
+// per-ray half-width M for every sphere:
+//   h  = od - C.d                       (3 fma; od = o.d per ray)
+//   ca = a|o|^2 - 2a o.C + a*k          (4 fma; k = |C|^2 - r2 from the host)
+//   D  = fma(h, h, -ca)
+// Error bound: with Hs >= (|o| + L) sqrt(a), L >= |C_k| + R_k,
+// |D - D_ref| <= 52.5u*Hs^2 <= 2^-47.3 Hs^2 (u = 2^-53), where D_ref =
+// disc_ref/4.  Rays with D >= T1 = 2^-36 Hs^2 are resolved: the reference's
+// disc > 0, and sa (v_rsq_f64 + one Newton step, <= 2^-45 relative) is within
+// 2^-29.3 Hs of its rounded sqrt, so |n - n_ref| <= 2^-29.29 Hs; a*t_ref lies
+// within u|n| of n_ref.  M = 2^-26 Hs (+ thr*2^-48 for the rounding of
+// thr = a*1e-4) leaves a factor 9.8 of slack.  D < -T2 = -2^-44 Hs^2 is a sure
+// miss; in between (grazing rays) the ray is ambiguous.  Root choice follows
+// hit_sphere: n1 if it may reach 1e-4 (a straddle is ambiguous), else n2.
+// Two winners closer than 2M are ambiguous, so a strictly smaller interval is
+// a strictly smaller t_ref (the reference keeps the first of equal t).
+// Non-finite o, d or Hs^2 > 2^1000 make the ray ambiguous up front.
+template <bool COUNT>
+__device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, const V3 d, double a, double two_a,
+                                               double four_a, bool fast, double rc2a, double& t_best, Cnt& cnt)
+{
+    const cdptr sc = (cdptr)kp.sph_cand;
     const double INF = dinf();
-    double blo = INF, bhi = INF;
+    const double od = fma(o.z, d.z, fma(o.y, d.y, o.x * d.x));
+    const double aoo = a * fma(o.z, o.z, fma(o.y, o.y, o.x * o.x));
+    const double m2a = -2.0 * a;
+    const double oax = m2a * o.x, oay = m2a * o.y, oaz = m2a * o.z;
+    // Hs >= (|o| + L) sqrt(a): |o|_1 >= |o|_2; v_rsq_f64 is within 2^-24
+    const double sqa = (a * __builtin_amdgcn_rsq(a)) * (1.0 + 0x1p-20);
+    const double Hs = ((fabs(o.x) + fabs(o.y)) + fabs(o.z) + kp.cand_lmax) * sqa;
+    const double Hs2 = Hs * Hs;
+    const double T1 = Hs2 * RT_CAND_T1, nT2 = Hs2 * -0x1p-44;
+    const double thr = a * 0.0001;
+    const double M = fma(thr, 0x1p-48, Hs * RT_CAND_M);
+    const double thrP = thr + M, thrM = thr - M, M2 = 2.0 * M;
+    double bn = INF;
     int bk = -1;
-    bool amb = false;
-    const double inv2a_m = inv2a * 0x1p-38;
+    // finite o, d, Hs^2 keep every D below finite; anything else takes the exact scan
+    bool amb = !(fast && Hs2 <= 0x1p1000);
     for (int k = 0; k < kp.ns_pad; k += 2) {
         double g[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = sg[4 * k + j];
+        for (int j = 0; j < 8; ++j) g[j] = sc[4 * k + j];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const double ocx = o.x - g[4 * h], ocy = o.y - g[4 * h + 1], ocz = o.z - g[4 * h + 2];
-            const double b = 2.0 * (ocx * d.x + ocy * d.y + ocz * d.z);
-            const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - g[4 * h + 3];
-            const double disc = b * b - four_a * c;
-            if (disc > 0) {
-                if (COUNT) cnt.c[RT_CNT_SPHERE_DISC] += 1;
-#ifndef RT_CAND_BRANCHY
-                // Straight-line: both roots, the acceptance logic as masks and
-                // the interval update as selects (no phi copies, no exec
-                // juggling).  Out-of-range disc (rsq invalid) -> ambiguous.
-                const bool inr = disc >= 0x1p-900 && disc <= 0x1p900;
-                // sa ~ sqrt(disc): v_rsq_f64 + one Newton step folded into
-                // sa = t + t*e/2, t = disc*r0, e = 1 - t*r0 (fma).
-                const double r0 = __builtin_amdgcn_rsq(disc);
-                const double tt = disc * r0;
-                const double sa = fma(tt * 0.5, fma(-tt, r0, 1.0), tt);
-                // one margin for both roots: (|b| + sa)/(2a) * 2^-38 bounds
-                // sa*inv2a*2^-39.7 + |q|*2^-50
-                const double M = (fabs(b) + sa) * inv2a_m;
-                const double q1 = (-b - sa) * inv2a, q2 = (sa - b) * inv2a;   // t1, t2
-                const bool c1 = q1 - M >= 0.0001, a1 = q1 + M >= 0.0001;      // surely / maybe >= 1e-4
-                const bool c2 = q2 - M >= 0.0001, a2 = q2 + M >= 0.0001;
-                const bool use2 = !a1 && c2;
-                const bool cand = inr && (c1 || use2);
-                const double q = c1 ? q1 : q2;
-                const double lo = q - M, hi = q + M;
-                const bool closer = cand && hi < blo;
-                amb = amb || !inr || (a1 && !c1) || (!a1 && !c2 && a2) || (cand && !closer && !(lo >= bhi));
-                blo = closer ? lo : blo;
-                bhi = closer ? hi : bhi;
-                bk = closer ? k + h : bk;
-#else
-                if (!(disc >= 0x1p-900 && disc <= 0x1p900)) {
-                    amb = true;
-                    continue;
-                }
-                const double r0 = __builtin_amdgcn_rsq(disc);
-                const double tt = disc * r0;
-                const double sa = fma(tt * 0.5, fma(-tt, r0, 1.0), tt);
-                const double M = (fabs(b) + sa) * inv2a_m;
-                double q = (-b - sa) * inv2a;              // near root t1
-                if (!(q - M >= 0.0001)) {
-                    if (q + M >= 0.0001) {                 // t1 straddles the 1e-4 threshold
-                        amb = true;
-                        continue;
-                    }
-                    q = (sa - b) * inv2a;                  // far root t2
-                    if (!(q - M >= 0.0001)) {
-                        if (q + M >= 0.0001) amb = true;
-                        continue;
-                    }
-                }
-                const double lo = q - M, hi = q + M;
-                const bool closer = hi < blo;
-                amb = amb || (!closer && !(lo >= bhi));
-                blo = closer ? lo : blo;
-                bhi = closer ? hi : bhi;
-                bk = closer ? k + h : bk;
-#endif
-            }
+        for (int e = 0; e < 2; ++e) {
+            const double cx = g[4 * e], cy = g[4 * e + 1], cz = g[4 * e + 2], kk = g[4 * e + 3];
+            const double h = fma(-cz, d.z, fma(-cy, d.y, fma(-cx, d.x, od)));
+            const double ca = fma(cz, oaz, fma(cy, oay, fma(cx, oax, fma(a, kk, aoo))));
+            const double D = fma(h, h, -ca);
+            const bool low = D < T1;                        // D finite here
+            const bool valid = !low;
+            amb = amb || (low && D >= nT2);
+            // sa ~ sqrt(D): v_rsq_f64 + one Newton step (sa = t + t*e/2)
+            const double r0 = __builtin_amdgcn_rsq(D);
+            const double tt = D * r0;
+            const double sa = fma(tt * 0.5, fma(-tt, r0, 1.0), tt);
+            const double n1 = -h - sa, n2 = sa - h;
+            const double n = n1 >= thrM ? n1 : n2;          // n1 may reach 1e-4: hit_sphere takes t1
+            const bool sure = n >= thrP;
+            amb = amb || (valid && !sure && n >= thrM);     // the chosen root straddles 1e-4
+            const bool cand = valid && sure;
+            const double diff = n - bn;
+            const bool closer = cand && diff < -M2;
+            amb = amb || (cand && !closer && fabs(diff) <= M2);
+            bn = closer ? n : bn;
+            bk = closer ? k + e : bk;
         }
     }
+    if (COUNT)
+        for (int k = 0; k < kp.ns; ++k) cnt.c[RT_CNT_SPHERE_DISC] += disc_positive(kp.sph[k], o, d, four_a) ? 1 : 0;
     double t = INF;
     int win = -1;
     if (!amb && bk >= 0) {
@@ -318,17 +345,7 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     }
     if (amb) {               // exact reference scan for this ray
         if (COUNT) cnt.c[RT_CNT_EXACT_RESCANS] += 1;
-        t = INF;
-        win = -1;
-        for (int k = 0; k < kp.ns_pad; ++k) {
-            double tk;
-            if (sphere_exact(sg[4 * k], sg[4 * k + 1], sg[4 * k + 2], sg[4 * k + 3], o, d, two_a, four_a, fast, rc2a,
-                             tk) &&
-                tk < t) {
-                t = tk;
-                win = k;
-            }
-        }
+        win = spheres_exact_scan(kp, o, d, two_a, four_a, fast, rc2a, t);
     }
     t_best = t;
     return win;
@@ -451,21 +468,18 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
     const double four_a = 4 * a;         // sphere.h:24
     const bool fast = two_a >= 0x1p-100 && two_a <= 0x1p100;
     const double rc2a = rcp_refined(two_a);
-    double inv2a;                        // RN(1 / two_a), candidate pass only
-    if (fast) inv2a = div_core(1.0, two_a, rc2a);
-    else inv2a = 1.0 / two_a;
     if (COUNT) {
         cnt.c[RT_CNT_CASTS] += 1;
         cnt.c[RT_CNT_SPHERE_TESTS] += (unsigned long long)kp.ns;
         cnt.c[RT_CNT_TRI_TESTS] += (unsigned long long)kp.nt;
     }
     double best;
-    int win = spheres_closest<COUNT>(kp, o, d, two_a, four_a, inv2a, fast, rc2a, best, cnt);
+    int win = spheres_closest<COUNT>(kp, o, d, a, two_a, four_a, fast, rc2a, best, cnt);
 #ifdef RT_DUP_SPHERES
     {
         double b2;
-        const int w2 = spheres_closest<COUNT>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, two_a, four_a,
-                                              inv2a, fast, rc2a, b2, cnt);
+        const int w2 = spheres_closest<COUNT>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, a, two_a,
+                                              four_a, fast, rc2a, b2, cnt);
         const bool f = opaque_false();
         best = f ? b2 : best;
         win = f ? w2 : win;
