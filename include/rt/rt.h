@@ -243,6 +243,14 @@ int rt_denoise_pack_async(int W, int H, const rt_frame* frame, float* color3, fl
  * for binary ops. */
 int rt_selftest_math(int op, const double* in, double* out, int n);
 
+/* Exhaustive check of the sampler's fast phi path (random_dir_no_norm,
+ * rtutility.h:196-200): for every rand() value r in [r0, r0 + n) (r < 2^31),
+ * sinf/cosf of (float)acos(2 r/2^31 - 1) from the fast path against the full
+ * portable path.  counts[0] = inputs that take the fallback, counts[1] =
+ * inputs whose fast result differs (0 is the correctness bar).  Synchronous,
+ * device 0. */
+int rt_verify_sampler_phi(unsigned long long r0, unsigned long long n, unsigned long long counts[2]);
+
 #ifdef __cplusplus
 }
 #endif

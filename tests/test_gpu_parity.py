@@ -114,6 +114,14 @@ def test_device_normalize_fast_path_is_ieee():
     assert same.all(), v[~same.all(1)][:4]
 
 
+def test_sampler_phi_fast_path_exhaustive():
+    """The fast phi path (phi_sincosf_fast) gives the full path's floats for
+    every one of the 2^31 rand() values, and falls back rarely."""
+    fb, bad = tipe_rt.verify_sampler_phi(0, 1 << 31)
+    assert bad == 0
+    assert fb < (1 << 31) // 2000
+
+
 def test_device_atan2_matches_oracle():
     o = oracle_ffi.oracle()
     rng = np.random.default_rng(21)

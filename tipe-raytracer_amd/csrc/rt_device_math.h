@@ -44,6 +44,10 @@ enum : int {
     // atan2 (fdlibm, sky mapping)
     KC_ATHI0, KC_ATHI1, KC_ATHI2, KC_ATHI3, KC_ATLO0, KC_ATLO1, KC_ATLO2, KC_ATLO3,
     KC_AT0, KC_AT1, KC_AT2, KC_AT3, KC_AT4, KC_AT5, KC_AT6, KC_AT7, KC_AT8, KC_AT9, KC_AT10, KC_PI_LO53,
+    // acos(t)/sqrt(1-t) on [0, 1], degree 13 (Chebyshev interpolant, relative
+    // error 2^-42.1 in FMA Horner): the sampler's fast phi path
+    KC_AC0, KC_AC1, KC_AC2, KC_AC3, KC_AC4, KC_AC5, KC_AC6, KC_AC7, KC_AC8, KC_AC9, KC_AC10, KC_AC11,
+    KC_AC12, KC_AC13,
     KC_COUNT
 };
 
@@ -70,6 +74,10 @@ __constant__ const double kC[KC_COUNT] = {
     3.33333333333329318027e-01, -1.99999999998764832476e-01, 1.42857142725034663711e-01, -1.11111104054623557880e-01,
     9.09088713343650656196e-02, -7.69187620504482999495e-02, 6.66107313738753120669e-02, -5.83357013379057348645e-02,
     4.97687799461593236017e-02, -3.65315727442169155270e-02, 1.62858201153657823623e-02, 0x1.1a62633145c07p-53,
+    0x1.921fb54442754p+0, -0x1.b7812aea8849fp-3, 0x1.6cbe3d540e1c7p-4, -0x1.a017c9f170088p-5,
+    0x1.13e462e97bdc4p-5, -0x1.8eee6d835d3f8p-6, 0x1.2fa02342d2e11p-6, -0x1.d62d02a699df8p-7,
+    0x1.5fc3eaba82359p-7, -0x1.d837e1419ed96p-8, 0x1.03cccf4b0779fp-8, -0x1.a5fa2f9ab0735p-10,
+    0x1.b5b26a8fad8b5p-12, -0x1.ac25f83fc9b71p-15,
 };
 
 // Scalar load of constant i (index laundered through b = opq0()).
@@ -238,6 +246,56 @@ __device__ __forceinline__ double pm_acos(double x)
         else res = (x - x) / (x - x);
     }
     return res;
+}
+
+// ---- sinf/cosf of (float)acos(x): the sampler's phi (rtutility.h:196-200) ---
+// Fast path of pm_sincosf((float)pm_acos(x), sp, cp) for x = 2v - 1 on the
+// 2^-30 grid.  Only the float phi reaches the image, and cos(phi) = x,
+// sin(phi) = sqrt(1 - x^2) are known, so:
+//   A  = sqrt(1 - |x|) * P(|x|)  (pi - that for x < 0)   |A - acos x| <= e1
+//   f  = (float)A, certain when A -+ e1 round to the same float (then
+//        pm_acos(x), within 1 ulp of acos x, rounds to f as well)
+//   dl = f - A (exact); with the true offset f - phi = dl + (A - phi),
+//   cos f = x cos dl - s sin dl,  sin f = s cos dl + x sin dl  (s = sin phi),
+//   evaluated to second order (|dl| <= 2^-22.3, the cubic terms < 2^-66),
+//   each certain when its value -+ its error bound rounds to one float.
+// Error bounds: P 2^-42.1 and sqrt 2^-45 relative, so
+// e1 = a0*2^-40 + 2^-49 (a0 = acos|x|; 2^-49 covers pi's rounding and the
+// subtraction); cos: e1 + 2^-48; sin: e1 + s*2^-44 + 2^-48.  Returns false
+// when any of the three roundings is not certain (about 1e-4 of the inputs;
+// x = -1 gives NaN and false), and the caller runs the full path.  All 2^31
+// inputs are checked against the full path on the GPU (rt_verify_sampler_phi).
+__device__ __forceinline__ bool phi_sincosf_fast(double x, float& sp, float& cp)
+{
+    const int b = opq0();
+    const double ax = fabs(x);
+    const double w = 1.0 - ax;                                 // exact on the grid
+    const double r0 = __builtin_amdgcn_rsq(w);
+    const double t0 = w * r0;
+    const double sw = fma(t0 * 0.5, fma(-t0, r0, 1.0), t0);    // sqrt(w), 2^-45
+    double p = KCV(b, KC_AC13);
+#pragma unroll
+    for (int j = 12; j >= 0; --j) p = fma(p, ax, KCV(b, KC_AC0 + j));
+    const double a0 = sw * p;                                  // acos(|x|)
+    const double A = x < 0.0 ? KCV(b, KC_PI) - a0 : a0;
+    const double e1 = fma(a0, 0x1p-40, 0x1p-49);
+    const float f = (float)(A - e1);
+    const bool ok1 = __float_as_uint(f) == __float_as_uint((float)(A + e1));
+    const double dl = (double)f - A;
+    const double q = fma(-x, x, 1.0);                          // 1 - x^2
+    const double r1 = __builtin_amdgcn_rsq(q);
+    const double t1 = q * r1;
+    const double s = fma(t1 * 0.5, fma(-t1, r1, 1.0), t1);     // sin(acos x), 2^-45
+    const double d2 = dl * dl;
+    const double C = fma(-s, dl, fma(-0.5 * x, d2, x));
+    const double S = fma(x, dl, fma(-0.5 * s, d2, s));
+    const double e2 = e1 + 0x1p-48;
+    const double e3 = fma(s, 0x1p-44, e2);
+    cp = (float)(C - e2);
+    sp = (float)(S - e3);
+    const bool ok2 = __float_as_uint(cp) == __float_as_uint((float)(C + e2));
+    const bool ok3 = __float_as_uint(sp) == __float_as_uint((float)(S + e3));
+    return ok1 && ok2 && ok3;
 }
 
 // ---- atan2 (oracle/pm_math.h pm_atan2; sky mapping only) -------------------

@@ -342,6 +342,14 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
         const SphGeo s = kp.sph[bk];
         if (sphere_exact(s.cx, s.cy, s.cz, s.r2, o, d, two_a, four_a, fast, rc2a, t)) win = bk;
         else amb = true;     // cannot happen within the bound; stay exact anyway
+#ifdef RT_DUP_WINNER
+        {
+            double t2;
+            const bool w2 = sphere_exact(s.cx, s.cy, s.cz, s.r2, v3(launder(o.x), launder(o.y), launder(o.z)), d,
+                                         two_a, four_a, fast, rc2a, t2);
+            if (opaque_false()) { t = t2; amb = !w2; }
+        }
+#endif
     }
     if (amb) {               // exact reference scan for this ray
         if (COUNT) cnt.c[RT_CNT_EXACT_RESCANS] += 1;
@@ -583,20 +591,26 @@ __device__ __forceinline__ V3 random_dir(Stream& st, Cnt& cnt)
     const double u = unit31(st.next31());
     const double v = unit31(st.next31());
     const double theta = 0x1.921fb54442d18p+2 * u;        // 2*PI*u
-    double phi = pm_acos(2 * v - 1);
-#ifdef RT_DUP_ACOS
-    { const double p2 = pm_acos(launder(2 * v - 1)); phi = opaque_false() ? p2 : phi; }
-#endif
+    const double xv = 2 * v - 1;                          // phi = acos(2v - 1): only (float)phi is used
     float st_, ct_, sp_, cp_;
+    if (!phi_sincosf_fast(xv, sp_, cp_)) {                // uncertain rounding (~1e-4): full path
+        const double phi = pm_acos(xv);
+        pm_sincosf((float)phi, sp_, cp_);
+    }
+#ifdef RT_DUP_ACOS
+    {
+        float a, c2;
+        const bool ok = phi_sincosf_fast(launder(xv), a, c2);
+        if (opaque_false()) { sp_ = a; cp_ = ok ? c2 : a; }
+    }
+#endif
     pm_sincosf((float)theta, st_, ct_);
-    pm_sincosf((float)phi, sp_, cp_);
 #ifdef RT_DUP_SINCOS
     {
-        float a, b, c2, d2;
+        float a, b;
         pm_sincosf(launder((float)theta), a, b);
-        pm_sincosf(launder((float)phi), c2, d2);
         const bool f = opaque_false();
-        st_ = f ? a : st_; ct_ = f ? b : ct_; sp_ = f ? c2 : sp_; cp_ = f ? d2 : cp_;
+        st_ = f ? a : st_; ct_ = f ? b : ct_;
     }
 #endif
     const V3 dir = v3((double)(ct_ * sp_), (double)(st_ * sp_), (double)cp_);
@@ -1116,6 +1130,36 @@ int launch_assemble(const double* gathered, long long rank_stride, int world, in
     hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, gathered,
                        rank_stride, world, tile_rows, rows_per_rank, W, H, out);
     return (int)hipGetLastError();
+}
+
+// Every sampler input r in [r0, r0 + n): phi_sincosf_fast against the full
+// path pm_sincosf((float)pm_acos(2 r/2^31 - 1)).  counts[0] += inputs that
+// fall back, counts[1] += inputs whose fast result differs (must stay 0).
+__global__ __launch_bounds__(256) void verify_phi_kernel(unsigned long long r0, unsigned long long n,
+                                                        unsigned long long* counts)
+{
+    const unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x;
+    bool fb = false, bad = false;
+    if (i < n) {
+        const double xv = 2 * unit31((uint32_t)(r0 + i)) - 1;
+        float sp, cp, s2, c2;
+        const bool ok = phi_sincosf_fast(xv, sp, cp);
+        pm_sincosf((float)pm_acos(xv), s2, c2);
+        fb = !ok;
+        bad = ok && (__float_as_uint(sp) != __float_as_uint(s2) || __float_as_uint(cp) != __float_as_uint(c2));
+    }
+    const unsigned long long nf = __popcll(__ballot(fb)), nb = __popcll(__ballot(bad));
+    if ((threadIdx.x & 63) == 0) {
+        if (nf) atomicAdd(counts, nf);
+        if (nb) atomicAdd(counts + 1, nb);
+    }
+}
+
+int launch_verify_phi(unsigned long long r0, unsigned long long n, unsigned long long* d_counts)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(verify_phi_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr, r0, n, d_counts);
+    return hipGetLastError();
 }
 
 int launch_selftest(int op, const double* d_in, double* d_out, int n, void* stream)
