@@ -149,10 +149,14 @@ __device__ __forceinline__ int pm_sincos(float x, double& s, double& c)
     const double kd = rint(xd * KCV(b, KC_TWO_OVER_PI));
     const double r = fma(-kd, KCV(b, KC_PIO2_1T), fma(-kd, KCV(b, KC_PIO2_1), xd));
     const double z = r * r;
-    const double ps = fma(z, fma(z, fma(z, fma(z, fma(z, KCV(b, KC_S6), KCV(b, KC_S5)), KCV(b, KC_S4)),
-                                        KCV(b, KC_S3)), KCV(b, KC_S2)), KCV(b, KC_S1));
-    const double pc = fma(z, fma(z, fma(z, fma(z, fma(z, KCV(b, KC_C6), KCV(b, KC_C5)), KCV(b, KC_C4)),
-                                        KCV(b, KC_C3)), KCV(b, KC_C2)), KCV(b, KC_C1));
+    // |z| == z (z >= +0): the abs modifier keeps each Horner step one VOP3
+    // v_fma_f64 with the SGPR coefficient as addend; without it the compiler
+    // picks v_fmac (tied VGPR addend) plus two v_mov of the coefficient.
+    const double za = fabs(z);
+    const double ps = fma(za, fma(za, fma(za, fma(za, fma(za, KCV(b, KC_S6), KCV(b, KC_S5)), KCV(b, KC_S4)),
+                                          KCV(b, KC_S3)), KCV(b, KC_S2)), KCV(b, KC_S1));
+    const double pc = fma(za, fma(za, fma(za, fma(za, fma(za, KCV(b, KC_C6), KCV(b, KC_C5)), KCV(b, KC_C4)),
+                                          KCV(b, KC_C3)), KCV(b, KC_C2)), KCV(b, KC_C1));
     s = fma(r * z, ps, r);
     c = fma(z * z, pc, fma(-0.5, z, 1.0));
     return (int)((long long)kd & 3);
@@ -204,9 +208,10 @@ __device__ __forceinline__ double div_core(double x, double d, double rc)   // |
 // ---- acos (fdlibm scheme) --------------------------------------------------
 __device__ __forceinline__ double pm_acos_R(int b, double z)
 {
-    const double p = z * fma(z, fma(z, fma(z, fma(z, fma(z, KCV(b, KC_PS5), KCV(b, KC_PS4)), KCV(b, KC_PS3)),
-                                          KCV(b, KC_PS2)), KCV(b, KC_PS1)), KCV(b, KC_PS0));
-    const double q = fma(z, fma(z, fma(z, fma(z, KCV(b, KC_QS4), KCV(b, KC_QS3)), KCV(b, KC_QS2)), KCV(b, KC_QS1)), 1.0);
+    const double za = fabs(z);                    // z >= +0 (see pm_sincos)
+    const double p = z * fma(za, fma(za, fma(za, fma(za, fma(za, KCV(b, KC_PS5), KCV(b, KC_PS4)), KCV(b, KC_PS3)),
+                                            KCV(b, KC_PS2)), KCV(b, KC_PS1)), KCV(b, KC_PS0));
+    const double q = fma(za, fma(za, fma(za, fma(za, KCV(b, KC_QS4), KCV(b, KC_QS3)), KCV(b, KC_QS2)), KCV(b, KC_QS1)), 1.0);
     return div_core(p, q, rcp_refined(q));   // q in [0.7, 1.1], p = +0 or >= 2^-70: exact
 }
 

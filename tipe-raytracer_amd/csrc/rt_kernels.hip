@@ -315,9 +315,10 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             const double h = fma(-cz, d.z, fma(-cy, d.y, fma(-cx, d.x, od)));
             const double ca = fma(cz, oaz, fma(cy, oay, fma(cx, oax, fma(a, kk, aoo))));
             const double D = fma(h, h, -ca);
-            const bool low = D < T1;                        // D finite here
-            const bool valid = !low;
-            amb = amb || (low && D >= nT2);
+            // D finite here.  The ambiguity tests use xor of nested conditions
+            // (a implies b: b && !a == a ^ b) so each comparison is issued once.
+            const bool valid = D >= T1;
+            amb = amb || (valid != (D >= nT2));             // -T2 <= D < T1: grazing
             // sa ~ sqrt(D): v_rsq_f64 + one Newton step (sa = t + t*e/2)
             const double r0 = __builtin_amdgcn_rsq(D);
             const double tt = D * r0;
@@ -325,11 +326,11 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             const double n1 = -h - sa, n2 = sa - h;
             const double n = n1 >= thrM ? n1 : n2;          // n1 may reach 1e-4: hit_sphere takes t1
             const bool sure = n >= thrP;
-            amb = amb || (valid && !sure && n >= thrM);     // the chosen root straddles 1e-4
+            amb = amb || (valid && (sure != (n >= thrM)));  // the chosen root straddles 1e-4
             const bool cand = valid && sure;
             const double diff = n - bn;
             const bool closer = cand && diff < -M2;
-            amb = amb || (cand && !closer && fabs(diff) <= M2);
+            amb = amb || (cand && fabs(diff) <= M2);        // (closer implies |diff| > M2)
             bn = closer ? n : bn;
             bk = closer ? k + e : bk;
         }
