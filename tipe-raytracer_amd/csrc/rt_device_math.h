@@ -80,8 +80,18 @@ __constant__ const double kC[KC_COUNT] = {
     0x1.b5b26a8fad8b5p-12, -0x1.ac25f83fc9b71p-15,
 };
 
-// Scalar load of constant i (index laundered through b = opq0()).
-#define KCV(b, i) (((cdptr)kC)[(b) + (i)])
+// Opaque per-call base of the constant table: each function takes one
+// (b = kcb()) and reads its coefficients at immediate offsets from it, so
+// neither the loads nor per-constant addresses are hoisted into long-lived
+// SGPRs (at most the table address itself stays live).
+__device__ __forceinline__ cdptr kcb()
+{
+    cdptr p = (cdptr)kC;
+    asm volatile("" : "+s"(p));
+    return p;
+}
+// Scalar load of constant i from a base b = kcb().
+#define KCV(b, i) ((b)[(i)])
 
 // ---- Philox4x32-10 (Random123 / rocrand_philox4x32_10 engine) -------------
 struct Philox {
@@ -144,7 +154,7 @@ __device__ __forceinline__ double unit31(uint32_t r) { return (double)r / 214748
 // ---- sin / cos of a float, evaluated in double, rounded to float ----------
 __device__ __forceinline__ int pm_sincos(float x, double& s, double& c)
 {
-    const int b = opq0();
+    const cdptr b = kcb();
     const double xd = (double)x;
     const double kd = rint(xd * KCV(b, KC_TWO_OVER_PI));
     const double r = fma(-kd, KCV(b, KC_PIO2_1T), fma(-kd, KCV(b, KC_PIO2_1), xd));
@@ -206,7 +216,7 @@ __device__ __forceinline__ double div_core(double x, double d, double rc)   // |
 }
 
 // ---- acos (fdlibm scheme) --------------------------------------------------
-__device__ __forceinline__ double pm_acos_R(int b, double z)
+__device__ __forceinline__ double pm_acos_R(cdptr b, double z)
 {
     const double za = fabs(z);                    // z >= +0 (see pm_sincos)
     const double p = z * fma(za, fma(za, fma(za, fma(za, fma(za, KCV(b, KC_PS5), KCV(b, KC_PS4)), KCV(b, KC_PS3)),
@@ -221,7 +231,7 @@ __device__ __forceinline__ double pm_acos(double x)
     // the operations of its own case (same values as the branchy form in
     // oracle/pm_math.h), but the wave runs one rational R(z), one sqrt and
     // one extra division instead of three divergent copies of them.
-    const int b = opq0();
+    const cdptr b = kcb();
     const double PIO2_HI = KCV(b, KC_PIO2_HI), PIO2_LO = KCV(b, KC_PIO2_LO), PI = KCV(b, KC_PI);
     const unsigned long long u = (unsigned long long)__double_as_longlong(x);
     const uint32_t hx = (uint32_t)(u >> 32);
@@ -272,7 +282,7 @@ __device__ __forceinline__ double pm_acos(double x)
 // inputs are checked against the full path on the GPU (rt_verify_sampler_phi).
 __device__ __forceinline__ bool phi_sincosf_fast(double x, float& sp, float& cp)
 {
-    const int b = opq0();
+    const cdptr b = kcb();
     const double ax = fabs(x);
     const double w = 1.0 - ax;                                 // exact on the grid
     const double r0 = __builtin_amdgcn_rsq(w);
@@ -304,7 +314,7 @@ __device__ __forceinline__ bool phi_sincosf_fast(double x, float& sp, float& cp)
 }
 
 // ---- atan2 (oracle/pm_math.h pm_atan2; sky mapping only) -------------------
-__device__ __forceinline__ double pm_atan_pos(int b, double a)
+__device__ __forceinline__ double pm_atan_pos(cdptr b, double a)
 {
     int id;
     double x = a;
@@ -329,7 +339,7 @@ __device__ __forceinline__ double pm_atan_pos(int b, double a)
 
 __device__ __forceinline__ double pm_atan2(double y, double x)
 {
-    const int b = opq0();
+    const cdptr b = kcb();
     const double pi = KCV(b, KC_PI), pi_lo = KCV(b, KC_PI_LO53), pio2 = KCV(b, KC_PIO2_HI);
     const double inf = __longlong_as_double(0x7ff0000000000000ll);
     if (x != x || y != y) return x + y;
@@ -354,7 +364,7 @@ __device__ __forceinline__ double pm_atan2(double y, double x)
 // ---- pow ---------------------------------------------------------------------
 __device__ __forceinline__ double pm_from_bits(unsigned long long b) { return __longlong_as_double((long long)b); }
 
-__device__ __forceinline__ double pm_log(int b, double x)
+__device__ __forceinline__ double pm_log(cdptr b, double x)
 {
     const unsigned long long u = (unsigned long long)__double_as_longlong(x);
     int e = (int)((u >> 52) & 0x7ff) - 1023;
@@ -371,7 +381,7 @@ __device__ __forceinline__ double pm_log(int b, double x)
     return ed * KCV(b, KC_LN2_HI) + (lm + ed * KCV(b, KC_LN2_LO));
 }
 
-__device__ __forceinline__ double pm_exp(int b, double t)
+__device__ __forceinline__ double pm_exp(cdptr b, double t)
 {
     if (t > 709.0) return __longlong_as_double(0x7ff0000000000000ll);
     if (t < -708.0) return 0.0;
@@ -402,7 +412,7 @@ __device__ __forceinline__ double pm_pow(double x, double y)
         }
         return n < 0 ? 1.0 / res : res;
     }
-    const int b = opq0();
+    const cdptr b = kcb();
     const double inf = __longlong_as_double(0x7ff0000000000000ll);
     if (x != x || y != y) return x + y;
     if (x == 0.0) return y > 0.0 ? 0.0 : inf;

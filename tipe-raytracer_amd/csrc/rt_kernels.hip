@@ -542,7 +542,7 @@ __device__ __forceinline__ Mat tri_material(const KParams& kp, int k, const V3 P
     index = index < 0 ? 0 : index;                       // reference UB -> clamp
     index = index >= kp.n_texels ? kp.n_texels - 1 : index;
     Mat res = load_mat(kp.texels + index);
-    const int b = opq0();
+    const cdptr b = kcb();
     if (m == 1) {
         res.emis = v3(1, 1, 1);
         res.es = KCV(b, KC_ES1);          // 1.85
@@ -569,7 +569,7 @@ __device__ __forceinline__ void sky_material(const KParams& kp, int idx, const S
 {
     const double ri = kp.sph_rinv[idx];
     const double dx = (hp.x - s.cx) * ri, dy = (hp.y - s.cy) * ri, dz = (hp.z - s.cz) * ri;
-    const int b = opq0();
+    const cdptr b = kcb();
     const double PI = KCV(b, KC_PI);
     const double theta = pm_acos(-dy);
     const double phi = pm_atan2(-dz, dx) + PI;
@@ -646,7 +646,7 @@ __device__ __forceinline__ double hue_to_rgb(double t1, double t2, double hue)
     if (hue > 1.0) hue -= 1.0;
     if (6.0 * hue < 1.0) return t1 + (t2 - t1) * 6.0 * hue;
     if (2.0 * hue < 1.0) return t2;
-    if (3.0 * hue < 2.0) return t1 + (t2 - t1) * (KCV(opq0(), KC_TWO_THIRDS) - hue) * 6.0;
+    if (3.0 * hue < 2.0) return t1 + (t2 - t1) * (KCV(kcb(), KC_TWO_THIRDS) - hue) * 6.0;
     return t1;
 }
 __device__ __forceinline__ V3 hsl_roundtrip(V3 rgb)
@@ -671,7 +671,7 @@ __device__ __forceinline__ V3 hsl_roundtrip(V3 rgb)
     if (s == 0.0) return v3(l, l, l);
     const double t2 = (l < 0.5) ? (l * (1.0 + s)) : (l + s - l * s);
     const double t1 = 2.0 * l - t2;
-    const double third = KCV(opq0(), KC_THIRD);                 // 1.0 / 3.0
+    const double third = KCV(kcb(), KC_THIRD);                 // 1.0 / 3.0
     return v3(hue_to_rgb(t1, t2, h + third), hue_to_rgb(t1, t2, h), hue_to_rgb(t1, t2, h - third));
 }
 
@@ -709,7 +709,7 @@ __device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const
 // and the next chain bounce always overwrites them; they are final when the
 // chain ends (first non-hole bounce, a miss, a light, or the last bounce).
 template <bool COUNT, bool BVH, bool SKY>
-__device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, Stream& st, double* acc, Cnt& cnt)
+__device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, Stream& st, double* acc, Cnt& cnt)
 {
     PathState<!BVH> ps{acc};
     ps.init();
@@ -792,6 +792,9 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, double AO, 
         }
         V3 rc = ps.rc();
         if (kp.useAO) {
+            // AO_intensity read here (laundered index): hoisted, pm_pow's
+            // exponent analysis ran and spilled once per sample without AO
+            const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
             const V3 em = muls(mat.emis, mat.es * 1.5 * AO);
             ps.set_inc(ps.inc() + mulv(em, rc));
             if (rc.x > 0.5 || rc.y > 0.5 || rc.z > 0.5) rc = mulv(mat.diff, muls(rc, 1.3));
@@ -886,7 +889,7 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
             const V3 dest = co + muls(dir, U[b + U_FOCUS]);
             const V3 no = co + v3(dx, dy, 0);
             const V3 rd = normalize(dest - no);
-            trace<COUNT, BVH, SKY>(kp, no, rd, U[b + U_AO], st, acc, cnt);
+            trace<COUNT, BVH, SKY>(kp, no, rd, st, acc, cnt);
             if (COUNT) {
                 cnt.c[RT_CNT_SAMPLES] += 1;
                 cnt.c[RT_CNT_RNG_DRAWS] += st.n;
