@@ -74,7 +74,7 @@ def cpu_baseline(p, scene_bundle, threads=12):
     import oracle_ffi
     o = oracle_ffi.oracle()
     canva = np.zeros((H, W, 3))
-    starts = [100, 300, 500, 700, 850]
+    starts = [100, 250, 400, 550, 700, 850]
     t0 = time.perf_counter()
     for lo in starts:
         rc = o.oracle_render_rows(C.byref(scene_bundle), C.byref(p), lo + threads - 1, lo, threads, 0,

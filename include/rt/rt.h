@@ -186,6 +186,8 @@ enum {
     RT_CNT_BVH_TRI_TESTS, /* triangles actually tested through the BVH
                              (GPU diagnostic; RT_CNT_TRI_TESTS keeps the
                              reference's brute-force count)              */
+    RT_CNT_BVH_LANE_SLOTS, /* 64 x wave-level BVH traversal steps (GPU
+                             diagnostic; bvh_nodes / this = SIMD efficiency) */
     RT_NCOUNTERS
 };
 /* Same traversal as rt_render_async, no frame; adds event counts into the

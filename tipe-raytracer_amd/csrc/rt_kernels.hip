@@ -420,7 +420,12 @@ __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3
     int node = 0, sp = 0;
     while (true) {
         const BvhNode4* nd = kp.bvh + node;
-        if (COUNT) cnt.c[RT_CNT_BVH_NODES] += 1;
+        if (COUNT) {
+            cnt.c[RT_CNT_BVH_NODES] += 1;
+            // one lane per wave step adds 64 lane slots
+            if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1)
+                cnt.c[RT_CNT_BVH_LANE_SLOTS] += 64;
+        }
         bool h[4];
         double tn[4];
 #pragma unroll
@@ -435,13 +440,13 @@ __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3
         }
         int next = -1;
         double tnext = 0.0;
+        unsigned lm = 0;                                 // hit leaf slots
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             if (!h[c]) continue;
             const int ch = nd->child[c], n = nd->count[c];
             if (n > 0) {
-                for (int k = ch; k < ch + n; ++k) tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
-                if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)n;
+                lm |= 1u << c;
             } else if (next < 0) {
                 next = ch;
                 tnext = tn[c];
@@ -455,6 +460,29 @@ __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3
                 stk[sp * 256] = (unsigned short)push;
                 ++sp;
             }
+        }
+        // The triangles of every hit leaf in one loop, one triangle per lane
+        // and iteration: the wave runs max-over-lanes iterations instead of
+        // one divergent loop per child slot.
+        int k = 0, kend = 0;
+        while (lm != 0u || k < kend) {
+            if (k >= kend) {
+                const int c = __ffs(lm) - 1;
+                lm &= lm - 1u;
+                k = nd->child[c];
+                kend = k + nd->count[c];
+                if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)(kend - k);
+            }
+            tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
+#ifdef RT_DUP_TRILEAF
+            {
+                double b2 = best;
+                int k2 = kind, w2 = win, o2 = win_orig;
+                tri_test<COUNT>(kp, k, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2);
+                if (opaque_false()) { best = b2; kind = k2; win = w2; win_orig = o2; }
+            }
+#endif
+            ++k;
         }
         if (next >= 0) {
             node = next;
