@@ -4,7 +4,9 @@
     python tools/bench_configs.py [--spp-scale F] [--only C3,C4]
 
 bench.py's headline is C2 only; this reports the mesh scenes beside it (the
-rows §8(f-2) acceleration targets).  Full 1200x900 frames at a reduced spp
+rows §8(f-2) acceleration targets) and C5's 4K frame (3840x2880, C3 scene;
+`full_frame_s_on_config_gpus_linear` divides by the config's GPU count,
+which the row tiling achieves up to the gather).  Full frames at a reduced spp
 (Msamples/s is spp-independent: pixels are independent and the per-sample
 work does not depend on S); kernel time from HIP events on the launch
 stream, events/sample from rt_count_async at 4 spp.
@@ -23,18 +25,18 @@ import torch  # noqa: E402  (before librt_hip.so)
 import tipe_rt  # noqa: E402
 from tipe_rt import scenes  # noqa: E402
 
-W, H = 1200, 900
-
 CONFIGS = {
-    # name: (mesh builder or None, spp measured, bounces, useAO, AO_intensity, full spp of the config)
-    "C2": (None, 200, 6, False, 2.5, 1000),
-    "C3": (scenes.pyramid_mesh, 200, 6, False, 2.5, 1000),
-    "C4": (scenes.tree_mesh, 16, 8, True, 2.5, 2000),
+    # name: (mesh builder or None, spp measured, bounces, useAO, AO_intensity, full spp, W, H, GPUs of the config)
+    "C2": (None, 200, 6, False, 2.5, 1000, 1200, 900, 1),
+    "C3": (scenes.pyramid_mesh, 200, 6, False, 2.5, 1000, 1200, 900, 1),
+    "C4": (scenes.tree_mesh, 16, 8, True, 2.5, 2000, 1200, 900, 4),
+    # C5: 4K frame of the C3 scene (SURVEY.md §8 config resolution), 5000 spp over 8 GPUs
+    "C5": (scenes.pyramid_mesh, 20, 6, False, 2.5, 5000, 3840, 2880, 8),
 }
 
 
 def run(name, spp_scale, dev, stream):
-    mesh_fn, spp, bounces, ao, ao_int, full_spp = CONFIGS[name]
+    mesh_fn, spp, bounces, ao, ao_int, full_spp, W, H, gpus = CONFIGS[name]
     spp = max(1, int(spp * spp_scale))
     spheres = scenes.cornell_spheres()
     if mesh_fn is None:
@@ -74,10 +76,12 @@ def run(name, spp_scale, dev, stream):
     ds.close()
     samples = W * H * spp
     rate = samples / (ms * 1e-3) / 1e6
-    return {"config": name, "triangles": nt, "spheres": len(spheres), "bounces": bounces, "ao": ao,
-            "spp_measured": spp, "kernel_ms": round(ms, 3), "wall_ms": round(wall * 1e3, 3),
+    return {"config": name, "width": W, "height": H, "triangles": nt, "spheres": len(spheres), "bounces": bounces,
+            "ao": ao, "spp_measured": spp, "kernel_ms": round(ms, 3), "wall_ms": round(wall * 1e3, 3),
             "kernel_msamples_per_s": round(rate, 3),
             "full_frame_s_at_config_spp": round(W * H * full_spp / (rate * 1e6), 2),
+            "config_gpus": gpus,
+            "full_frame_s_on_config_gpus_linear": round(W * H * full_spp / (rate * 1e6) / gpus, 2),
             "events_per_sample": {k: round(cnt[i] / max(cnt[0], 1), 3) for i, k in enumerate(tipe_rt.COUNTER_NAMES)}}
 
 
