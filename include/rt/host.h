@@ -10,6 +10,8 @@
  *                          loader cannot read: texture.h:182 strstr(NULL))
  *   rt_host_read_ppm      P3 reader              texture.h:145-173
  *   rt_host_write_ppm     P3 writer              main.c:457-465
+ *   rt_host_cuda_materials per-mesh materials of main_cuda.cu's loader
+ *                                                triangle.hu:94-105
  *
  * All functions return RT_OK or a negative RT_E* code (rt.h); nothing exits.
  */
@@ -49,6 +51,12 @@ void rt_host_free_mesh(rt_mesh* m);
  * flat texture of its Kd (alpha 1, reflectionStrength Ns/100 as
  * triangle.hu:104-105), sized like the others (1x1 if none has a map). */
 int rt_host_load_textures(const rt_mesh* mesh, int kd_fallback, rt_material** mat_list, int* tw, int* th);
+
+/* RT_SEM_CUDA materials (rt.h): each triangle's rt_triangle.mat becomes its
+ * material's {Kd, black, 0, Ns/100} as main_cuda.cu's assimp loader builds
+ * it per mesh (triangle.hu:94-105: float Kd and shininess, reflection =
+ * (double)(shininess/100)), with alpha 1. */
+void rt_host_cuda_materials(rt_mesh* mesh);
 
 /* P3 PPM reader: returns w*h*3 values as read (rows as stored, top first). */
 int rt_host_read_ppm(const char* path, int* w, int* h, int* maxval, int** values);

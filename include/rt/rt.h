@@ -82,7 +82,31 @@ typedef struct rt_params {
     unsigned long long seed;           /* Philox key                             */
     int accel;                         /* RT_ACCEL_*: triangle traversal          */
     int sky_mode;                      /* RT_SKY_*                                */
+    int semantics;                     /* RT_SEM_*: whose integrator               */
 } rt_params;
+
+/* rt_params.semantics.  MAIN_C (default) is main.c, the authoritative CPU
+ * path.  CUDA is main_cuda.cu's integrator, the reference's
+ * GPU path (§8f, an optional fidelity mode):
+ *   - tracer main_cuda.cu:86-141: a pre-pass cast returns emitters as
+ *     hsl_to_rgb(rgb_to_hsl(emission) with L and S x1.20) and misses as 0; the
+ *     bounce loop has no alpha holes, refraction or textures, no x1.3
+ *     brightening; albedo/normal are the pre-pass hit's;
+ *   - hit_sphere sphere.hu:27-45 accepts t1 >= 0, then t2 >= 0.001;
+ *     hit_triangle triangle.hu:247-270 uses 1e-5 for dst/u/v/w;
+ *   - closest_hit main_cuda.cu:23-59 skips the triangles when the ray misses
+ *     their bounding box (hit_BBox, triangle.hu:42-59; one mesh = all the
+ *     triangles) and gives a triangle its own rt_triangle.mat (the CUDA
+ *     loader's per-mesh material: Kd, reflection Ns/100, triangle.hu:104-105);
+ *   - fill main_cuda.cu:152-156: jitter (i + 0.5 + U(-0.5, 0.5)) / (W - 1);
+ *     focus, aperture and AO_intensity are doubles (compat_int_truncation is
+ *     ignored), sky_mode must be OFF.
+ * The draws come from the same RT_RNG_PHILOX stream and the same portable
+ * sinf/cosf/acos (curand XORWOW and the __cosf/__sinf intrinsics of the CUDA
+ * build are NVIDIA-specific and not reproduced), so CUDA-mode images match
+ * the oracle's restatement of main_cuda.cu bit for bit, not NVIDIA output. */
+#define RT_SEM_MAIN_C 0
+#define RT_SEM_CUDA   1
 
 /* rt_params.sky_mode.  OFF is main.c as shipped (the sky branch of
  * closest_hit is commented out, main.c:64-71).  LAST_SPHERE enables that

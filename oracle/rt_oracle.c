@@ -60,6 +60,8 @@ typedef struct ctx {
     double AO;
     int rng, portable;
     int sky;                 /* rt.h RT_SKY_LAST_SPHERE with a sky table */
+    int cuda;                /* rt.h RT_SEM_CUDA: main_cuda.cu's integrator */
+    rt_point3 bb_lo, bb_hi;  /* CUDA mode: the triangles' bounding box */
     uint64_t seed;
     uint32_t pixel, sample, n;
     uint32_t block[4];
@@ -202,8 +204,14 @@ static oracle_hit hit_sphere(ctx* c, rt_point3 center, double radius, rt_ray r)
     return h;
 }
 
-/* hit_triangle, mesh.h:70-94 (one-sided, eps 1e-6 / 1e-7) */
+/* hit_triangle, mesh.h:70-94 (one-sided, eps 1e-6 / 1e-7); the CUDA path's
+ * triangle.hu:247-270 is the same arithmetic with eps 1e-5 for dst/u/v/w */
+static oracle_hit hit_triangle_eps(ctx* c, const rt_triangle* tri, rt_ray r, double eps);
 static oracle_hit hit_triangle(ctx* c, const rt_triangle* tri, rt_ray r)
+{
+    return hit_triangle_eps(c, tri, r, 0.0000001);
+}
+static oracle_hit hit_triangle_eps(ctx* c, const rt_triangle* tri, rt_ray r, double eps)
 {
     oracle_hit h;
     memset(&h, 0, sizeof h);
@@ -219,7 +227,7 @@ static oracle_hit hit_triangle(ctx* c, const rt_triangle* tri, rt_ray r)
     double u = dot(edgeAC, dao) * invDet;
     double v = -dot(edgeAB, dao) * invDet;
     double w = 1 - u - v;
-    h.didHit = det >= 1E-6 && dst >= 0.0000001 && u >= 0.0000001 && v >= 0.0000001 && w >= 0.0000001;
+    h.didHit = det >= 1E-6 && dst >= eps && u >= eps && v >= eps && w >= eps;
     h.hitPoint = add(r.origin, mul_s(r.dir, dst));
     h.normal = normalize(normalVect);
     h.dst = dst;
@@ -335,7 +343,87 @@ static oracle_hit closest_hit(ctx* c, rt_ray r, int count_tex)
     return best;
 }
 
-/* ambient_occlusion, main.c:94-116 (nbSamples = 1) */
+/* ---- CUDA path (rt.h RT_SEM_CUDA) ----------------------------------------- */
+/* hit_sphere, sphere.hu:13-47: the same discriminant and roots as sphere.h,
+ * accepting t1 >= 0, then t2 >= 0.001 */
+static oracle_hit hit_sphere_cuda(ctx* c, rt_point3 center, double radius, rt_ray r)
+{
+    oracle_hit h;
+    memset(&h, 0, sizeof h);
+    if (c) c->cnt[RT_CNT_SPHERE_TESTS]++;
+    rt_vec3 oc = sub(r.origin, center);
+    double a = dot(r.dir, r.dir);
+    double b = 2.0 * dot(oc, r.dir);
+    double cc = dot(oc, oc) - radius * radius;
+    double disc = b * b - 4 * a * cc;
+    if (disc > 0) {
+        if (c) c->cnt[RT_CNT_SPHERE_DISC]++;
+        double t1 = (-b - sqrt(disc)) / (2 * a);
+        if (t1 >= 0) {
+            h.didHit = 1;
+            h.dst = t1;
+            h.hitPoint = ray_at(r, t1);
+            h.normal = normalize(sub(ray_at(r, t1), center));
+            return h;
+        }
+        double t2 = (-b + sqrt(disc)) / (2 * a);
+        if (t2 >= 0.001) {
+            h.didHit = 1;
+            h.dst = t2;
+            h.hitPoint = ray_at(r, t2);
+            h.normal = normalize(sub(ray_at(r, t2), center));
+            return h;
+        }
+    }
+    return h;
+}
+
+/* hit_BBox, triangle.hu:42-59 (CUDA min/max on doubles are fmin/fmax) */
+static int hit_bbox_cuda(const ctx* c, rt_ray r)
+{
+    double tmin[3], tmax[3];
+    for (int k = 0; k < 3; k++) {
+        double t1 = (c->bb_lo.e[k] - r.origin.e[k]) / r.dir.e[k];
+        double t2 = (c->bb_hi.e[k] - r.origin.e[k]) / r.dir.e[k];
+        tmin[k] = fmin(t1, t2);
+        tmax[k] = fmax(t1, t2);
+    }
+    return fmin(fmin(tmax[0], tmax[1]), tmax[2]) - fmax(fmax(tmin[0], tmin[1]), tmin[2]) > 0;
+}
+
+/* closest_hit, main_cuda.cu:23-59: spheres, then (if the ray meets the mesh
+ * box) the triangles, each with its own material (the CUDA loader's per-mesh
+ * material, triangle.hu:104-105) */
+static oracle_hit closest_hit_cuda(ctx* c, rt_ray r)
+{
+    const rt_scene* sc = c->sc;
+    oracle_hit best;
+    memset(&best, 0, sizeof best);
+    best.dst = INFINITY;
+    c->cnt[RT_CNT_CASTS]++;
+    for (int i = 0; i < sc->nbSpheres; i++) {
+        const rt_sphere* s = &sc->sphere_list[i];
+        oracle_hit h = hit_sphere_cuda(c, s->center, s->radius, r);
+        if (h.didHit && h.dst < best.dst) {
+            best = h;
+            best.mat = s->mat;
+        }
+    }
+    if (sc->nbTriangles > 0 && hit_bbox_cuda(c, r)) {
+        for (int i = 0; i < sc->nbTriangles; i++) {
+            const rt_triangle* tri = &sc->triangle_list[i];
+            oracle_hit h = hit_triangle_eps(c, tri, r, 0.00001);
+            if (h.didHit && h.dst < best.dst) {
+                best = h;
+                best.mat = tri->mat;
+            }
+        }
+    }
+    return best;
+}
+
+/* ambient_occlusion, main.c:94-116 (nbSamples = 1); main_cuda.cu:61-84 is
+ * the same with its own closest_hit */
 static rt_color ambient_occlusion(ctx* c, rt_vec3 point, rt_vec3 normal, double AO_intensity)
 {
     const int nbSamples = 1;
@@ -344,7 +432,7 @@ static rt_color ambient_occlusion(ctx* c, rt_vec3 point, rt_vec3 normal, double 
         rt_vec3 randomDir = random_dir_no_norm(c);
         rt_vec3 hemisphereDir = add(normal, randomDir);
         rt_ray occlusionRay = {point, normalize(hemisphereDir)};
-        oracle_hit oh = closest_hit(c, occlusionRay, 0);
+        oracle_hit oh = c->cuda ? closest_hit_cuda(c, occlusionRay) : closest_hit(c, occlusionRay, 0);
         if (oh.didHit) {
             double distance = length(sub(oh.hitPoint, point));
             double attenuation = distance / oh.dst;
@@ -503,6 +591,58 @@ static void tracer(ctx* c, rt_ray r, rt_color out[3])
     out[2] = normal_color;
 }
 
+/* tracer, main_cuda.cu:86-141.  The pre-pass cast returns emitters (HSL
+ * round trip with L and S x1.20) and misses (0); the bounce loop then starts
+ * from the same ray; albedo/normal are the pre-pass hit's (the function's
+ * outer hitInfo, main_cuda.cu:140). */
+static void tracer_cuda(ctx* c, rt_ray r, rt_color out[3])
+{
+    oracle_hit first = closest_hit_cuda(c, r);
+    if (first.didHit) {
+        if (first.mat.emissionStrength > 0) {
+            rt_color HSL = rgb_to_hsl(first.mat.emissionColor);
+            HSL.e[2] *= 1.20;
+            HSL.e[1] *= 1.20;
+            rt_color newCol = hsl_to_rgb(HSL);
+            out[0] = newCol;
+            out[1] = newCol;
+            out[2] = first.normal;
+            return;
+        }
+    } else {
+        out[0] = out[1] = out[2] = v3(0, 0, 0);
+        return;
+    }
+    rt_color incomingLight = v3(0, 0, 0);
+    rt_color rayColor = v3(1, 1, 1);
+    for (int i = 0; i < c->B; i++) {
+        oracle_hit h = closest_hit_cuda(c, r);
+        if (h.didHit) {
+            rt_material mat = h.mat;
+            r.origin = h.hitPoint;
+            rt_vec3 diffuse_dir = normalize(add(h.normal, random_dir_no_norm(c)));
+            rt_vec3 reflected_dir = sub(r.dir, mul_s(h.normal, 2 * dot(r.dir, h.normal)));
+            r.dir = lerp(diffuse_dir, reflected_dir, mat.reflectionStrength);
+            if (c->useAO) {
+                rt_color emittedLight = mul_s(mat.emissionColor, mat.emissionStrength * 1.5 * c->AO);
+                incomingLight = add(incomingLight, mul(emittedLight, rayColor));
+                rayColor = mul(mat.diffuseColor, rayColor);
+                rt_color occlusion = ambient_occlusion(c, h.hitPoint, h.normal, c->AO);
+                rayColor = mul(rayColor, occlusion);
+            } else {
+                rt_color emittedLight = mul_s(mat.emissionColor, mat.emissionStrength);
+                incomingLight = add(incomingLight, mul(emittedLight, rayColor));
+                rayColor = mul(mat.diffuseColor, rayColor);
+            }
+        } else {
+            break;
+        }
+    }
+    out[0] = incomingLight;
+    out[1] = first.mat.diffuseColor;
+    out[2] = first.normal;
+}
+
 /* ------------------------------------------------------------------------ */
 /* camera, camera.h:21-55; resolve, rtutility.h:56-71                        */
 /* ------------------------------------------------------------------------ */
@@ -560,6 +700,19 @@ static void init_ctx(ctx* c, const band* b)
     c->portable = b->portable;
     c->sky = b->p->sky_mode == RT_SKY_LAST_SPHERE && b->sc->sky_mat_list && b->sc->nbSpheres > 0;
     c->seed = b->p->seed;
+    c->cuda = b->p->semantics == RT_SEM_CUDA;
+    if (c->cuda && b->sc->nbTriangles > 0) {           /* load_geometry_data's box, triangle.hu:142-156 */
+        const rt_triangle* t0 = &b->sc->triangle_list[0];
+        c->bb_lo = t0->A;
+        c->bb_hi = t0->A;
+        for (int i = 0; i < b->sc->nbTriangles; i++) {
+            const rt_triangle* t = &b->sc->triangle_list[i];
+            for (int k = 0; k < 3; k++) {
+                c->bb_lo.e[k] = fmin(c->bb_lo.e[k], fmin(t->A.e[k], fmin(t->B.e[k], t->C.e[k])));
+                c->bb_hi.e[k] = fmax(c->bb_hi.e[k], fmax(t->A.e[k], fmax(t->B.e[k], t->C.e[k])));
+            }
+        }
+    }
 }
 
 static void* band_worker(void* arg)
@@ -584,13 +737,20 @@ static void* band_worker(void* arg)
                     c.sample = (uint32_t)x;
                     c.n = 0;
                     c.cnt[RT_CNT_SAMPLES]++;
-                    double u = ((double)i + random_double(&c, -0.5, 0.5)) / (W - 1);
-                    double v = ((double)j + random_double(&c, -0.5, 0.5)) / (H - 1);
+                    double u, v;
+                    if (c.cuda) {                      /* main_cuda.cu:152-153 */
+                        u = ((double)i + 0.5 + random_double(&c, -0.5, 0.5)) / (W - 1);
+                        v = ((double)j + 0.5 + random_double(&c, -0.5, 0.5)) / (H - 1);
+                    } else {                           /* main.c:265-266 */
+                        u = ((double)i + random_double(&c, -0.5, 0.5)) / (W - 1);
+                        v = ((double)j + random_double(&c, -0.5, 0.5)) / (H - 1);
+                    }
                     double dx = random_double(&c, -0.5, 0.5) * b->ox;
                     double dy = random_double(&c, -0.5, 0.5) * b->oy;
                     rt_ray r = get_ray(u, v, &p->cam, b->focus, dx, dy);
                     rt_color smp[3];
-                    tracer(&c, r, smp);
+                    if (c.cuda) tracer_cuda(&c, r, smp);
+                    else tracer(&c, r, smp);
                     part[0] = add(part[0], smp[0]);
                     part[1] = add(part[1], smp[1]);
                     part[2] = add(part[2], smp[2]);
@@ -621,6 +781,8 @@ static int validate(const rt_scene* sc, const rt_params* p)
     if (p->largeur_image < 1 || p->hauteur_image < 1 || p->nbRayonParPixel < 1 || p->nbRebondMax < 0)
         return RT_EINVAL;
     if (p->rng != RT_RNG_GLIBC && p->rng != RT_RNG_PHILOX) return RT_EINVAL;
+    if (p->semantics != RT_SEM_MAIN_C && p->semantics != RT_SEM_CUDA) return RT_EINVAL;
+    if (p->semantics == RT_SEM_CUDA && p->sky_mode != RT_SKY_OFF) return RT_EINVAL;
     if (sc->nbSpheres < 0 || sc->nbTriangles < 0) return RT_EINVAL;
     if (sc->nbSpheres > 0 && !sc->sphere_list) return RT_EINVAL;
     if (sc->nbTriangles > 0) {
@@ -645,7 +807,7 @@ int oracle_render_rows(const rt_scene* scene, const rt_params* params, int row_h
 
     double focus = params->focus_distance, ox = params->ouverture_x, oy = params->ouverture_y;
     double AO = params->AO_intensity;
-    if (params->compat_int_truncation) {   /* ThreadData int fields, main.c:42-43 */
+    if (params->compat_int_truncation && params->semantics != RT_SEM_CUDA) {   /* ThreadData int fields, main.c:42-43 */
         focus = (double)(int)focus;
         ox = (double)(int)ox;
         oy = (double)(int)oy;
@@ -703,6 +865,10 @@ int oracle_render_rows(const rt_scene* scene, const rt_params* params, int row_h
 /* ------------------------------------------------------------------------ */
 oracle_hit oracle_hit_sphere(rt_point3 center, double radius, rt_ray r) { return hit_sphere(NULL, center, radius, r); }
 oracle_hit oracle_hit_triangle(const rt_triangle* tri, rt_ray r) { return hit_triangle(NULL, tri, r); }
+oracle_hit oracle_hit_sphere_cuda(rt_point3 center, double radius, rt_ray r)
+{
+    return hit_sphere_cuda(NULL, center, radius, r);
+}
 rt_material oracle_tri_uvmapping(const rt_triangle* tri, const oracle_hit* h, const rt_material* mat_list, int tw,
                                  int th, int tri_index, const int* quelMatPourTri)
 {

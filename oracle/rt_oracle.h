@@ -44,6 +44,7 @@ void oracle_set_math(int mode);
 /* Leaf functions (for parity against the compiled reference headers). */
 oracle_hit oracle_hit_sphere(rt_point3 center, double radius, rt_ray r);
 oracle_hit oracle_hit_triangle(const rt_triangle* tri, rt_ray r);
+oracle_hit oracle_hit_sphere_cuda(rt_point3 center, double radius, rt_ray r);   /* sphere.hu:13-47 */
 rt_material oracle_tri_uvmapping(const rt_triangle* tri, const oracle_hit* h,
                                  const rt_material* mat_list, int tw, int th,
                                  int tri_index, const int* quelMatPourTri);

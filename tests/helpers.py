@@ -63,11 +63,12 @@ def tree_scene(move=scenes.TREE_MOVE):
 
 
 def params(W, H, spp, bounces, use_ao=False, ao=2.5, rng=RT_RNG_PHILOX, seed=1010, compat=1, cam=None,
-           aperture=(0.0, 0.0), focus=3.0, chunks=1, accel=0, sky_mode=0):
+           aperture=(0.0, 0.0), focus=3.0, chunks=1, accel=0, sky_mode=0, semantics=0):
     if cam is None:
         cam = readme_camera_oracle()
     return tipe_rt.make_params(W, H, spp, bounces, cam, focus=focus, aperture=aperture, use_ao=use_ao, ao=ao,
-                               seed=seed, rng=rng, compat=compat, chunks=chunks, accel=accel, sky_mode=sky_mode)
+                               seed=seed, rng=rng, compat=compat, chunks=chunks, accel=accel, sky_mode=sky_mode,
+                               semantics=semantics)
 
 
 def oracle_render(bundle, p, row_hi=None, row_lo=0, nthreads=1, counters=False):

@@ -45,6 +45,8 @@ def oracle():
         lib.oracle_set_math.argtypes = [C.c_int]
         lib.oracle_hit_sphere.argtypes = [Vec3, C.c_double, Ray]
         lib.oracle_hit_sphere.restype = OracleHit
+        lib.oracle_hit_sphere_cuda.argtypes = [Vec3, C.c_double, Ray]
+        lib.oracle_hit_sphere_cuda.restype = OracleHit
         lib.oracle_hit_triangle.argtypes = [P(Triangle), Ray]
         lib.oracle_hit_triangle.restype = OracleHit
         lib.oracle_tri_uvmapping.argtypes = [P(Triangle), P(OracleHit), P(Material), C.c_int, C.c_int,

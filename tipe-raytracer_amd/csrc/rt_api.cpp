@@ -98,6 +98,10 @@ int validate_params(const rt_params* p)
     if (p->accel != RT_ACCEL_AUTO && p->accel != RT_ACCEL_NONE) return fail(RT_EINVAL, "unknown accel %d", p->accel);
     if (p->sky_mode != RT_SKY_OFF && p->sky_mode != RT_SKY_LAST_SPHERE)
         return fail(RT_EINVAL, "unknown sky_mode %d", p->sky_mode);
+    if (p->semantics != RT_SEM_MAIN_C && p->semantics != RT_SEM_CUDA)
+        return fail(RT_EINVAL, "unknown semantics %d", p->semantics);
+    if (p->semantics == RT_SEM_CUDA && p->sky_mode != RT_SKY_OFF)
+        return fail(RT_EINVAL, "sky_mode needs RT_SEM_MAIN_C (main_cuda.cu has no sky)");
     if ((unsigned long long)p->largeur_image * (unsigned long long)p->hauteur_image > 0xffffffffull)
         return fail(RT_EUNSUPPORTED, "pixel index exceeds the 32-bit Philox counter word");
     return RT_OK;
@@ -132,6 +136,8 @@ struct rt_device_scene {
     DevMat* texels = nullptr;
     BvhNode4* bvh = nullptr;         // 4-wide BVH; null: no BVH (few triangles)
     DevMat* sky = nullptr;           // sky texels (scene->sky_mat_list), or null
+    DevMat* tri_mat = nullptr;       // rt_triangle.mat per triangle (RT_SEM_CUDA)
+    double cbb[6] = {0, 0, 0, 0, 0, 0};   // triangles' box (RT_SEM_CUDA hit_BBox)
     double* sph_rinv = nullptr;      // 1/radius per sphere
     int sky_w = 0, sky_h = 0;
     int* tri_orig = nullptr;         // leaf order -> caller's triangle index
@@ -160,6 +166,7 @@ void free_scene(rt_device_scene* s)
     (void)hipFree(s->texels);
     (void)hipFree(s->bvh);
     (void)hipFree(s->sky);
+    (void)hipFree(s->tri_mat);
     (void)hipFree(s->sph_rinv);
     (void)hipFree(s->tri_orig);
     delete s;
@@ -197,6 +204,9 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.texels = sc->texels;
     kp.tri_orig = sc->tri_orig;
     kp.sph_rinv = sc->sph_rinv;
+    kp.tri_mat = sc->tri_mat;
+    kp.cuda = p->semantics == RT_SEM_CUDA ? 1 : 0;
+    for (int i = 0; i < 6; ++i) kp.cbb[i] = sc->cbb[i];
     if (p->sky_mode == RT_SKY_LAST_SPHERE && sc->sky && sc->ns > 0) {
         kp.sky = sc->sky;
         kp.sky_w = sc->sky_w;
@@ -219,7 +229,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
         uni[U_CAM_C + i] = p->cam.coin_bas_gauche.e[i];
     }
     double focus = p->focus_distance, ox = p->ouverture_x, oy = p->ouverture_y, AO = p->AO_intensity;
-    if (p->compat_int_truncation) {     // ThreadData int fields, main.c:42-43
+    if (p->compat_int_truncation && p->semantics != RT_SEM_CUDA) {   // ThreadData int fields, main.c:42-43
         focus = (double)(int)focus;
         ox = (double)(int)ox;
         oy = (double)(int)oy;
@@ -404,6 +414,18 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
             sky.push_back(to_dev(scene->sky_mat_list[i]));
     std::vector<TriGeo> tri((size_t)scene->nbTriangles);
     std::vector<TriTex> tex((size_t)scene->nbTriangles);
+    std::vector<DevMat> tri_mat((size_t)scene->nbTriangles);
+    double cbb[6] = {0, 0, 0, 0, 0, 0};
+    if (scene->nbTriangles > 0) {                    // load_geometry_data's box, triangle.hu:142-156
+        for (int a = 0; a < 3; ++a) cbb[a] = cbb[3 + a] = scene->triangle_list[0].A.e[a];
+        for (int i = 0; i < scene->nbTriangles; ++i) {
+            const rt_triangle& t = scene->triangle_list[i];
+            for (int a = 0; a < 3; ++a) {
+                cbb[a] = std::fmin(cbb[a], std::fmin(t.A.e[a], std::fmin(t.B.e[a], t.C.e[a])));
+                cbb[3 + a] = std::fmax(cbb[3 + a], std::fmax(t.A.e[a], std::fmax(t.B.e[a], t.C.e[a])));
+            }
+        }
+    }
     for (int i = 0; i < scene->nbTriangles; ++i) {
         const rt_triangle& t = scene->triangle_list[i];
         const double abx = t.B.e[0] - t.A.e[0], aby = t.B.e[1] - t.A.e[1], abz = t.B.e[2] - t.A.e[2];
@@ -436,6 +458,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         x.ucv = t.uvC.v;
         x.mat = scene->quelMatPourTri[i];
         x.pad = 0;
+        tri_mat[i] = to_dev(t.mat);
     }
     // Triangle BVH (rt_bvh.cpp) over scenes with more than 32 triangles; the
     // triangle arrays are then stored in leaf order.  r_scene bounds every
@@ -455,12 +478,15 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         if (std::isfinite(r) && build_bvh(tri.data(), scene->nbTriangles, r, bvh)) {
             std::vector<TriGeo> tri2(tri.size());
             std::vector<TriTex> tex2(tex.size());
+            std::vector<DevMat> mat2(tri_mat.size());
             for (size_t k = 0; k < tri.size(); ++k) {
                 tri2[k] = tri[(size_t)bvh.order[k]];
                 tex2[k] = tex[(size_t)bvh.order[k]];
+                mat2[k] = tri_mat[(size_t)bvh.order[k]];
             }
             tri.swap(tri2);
             tex.swap(tex2);
+            tri_mat.swap(mat2);
         }
     }
     std::vector<DevMat> texels;
@@ -476,6 +502,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->ns = scene->nbSpheres;
     ds->ns_pad = ns_pad;
     ds->cand_lmax = cand_lmax;
+    for (int i = 0; i < 6; ++i) ds->cbb[i] = cbb[i];
     ds->nt = scene->nbTriangles;
     ds->tw = scene->nbTriangles > 0 ? scene->tex_width : 1;
     ds->th = scene->nbTriangles > 0 ? scene->tex_height : 1;
@@ -490,7 +517,8 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_cand, cand)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
         (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels)) ||
         (rc = upload(&ds->bvh, bvh.nodes4)) || (rc = upload(&ds->tri_orig, bvh.order)) ||
-        (rc = upload(&ds->sky, sky)) || (rc = upload(&ds->sph_rinv, sph_rinv))) {
+        (rc = upload(&ds->sky, sky)) || (rc = upload(&ds->sph_rinv, sph_rinv)) ||
+        (rc = upload(&ds->tri_mat, tri_mat))) {
         free_scene(ds);
         return rc;
     }

@@ -15,6 +15,7 @@
 //   int     [nt]           triangle arrays are then in leaf order and
 //                          tri_orig maps back to the caller's order
 //   DevMat  [nm*th*tw]     texel table (reference `material` records)
+//   DevMat  [nt]           rt_triangle.mat per triangle (RT_SEM_CUDA materials)
 // Per launch: a 18-double uniform block (camera, focus, aperture, AO, W-1,
 // H-1) read through the scalar unit where used, and, when the samples of a
 // pixel are split over P chunks, a [P][pixels][9] partial-sum scratch.
@@ -74,6 +75,9 @@ struct KParams {
     const BvhNode4* bvh;     // 4-wide triangle BVH (rt_bvh.h), or null: brute-force scan
     const int* tri_orig;     // triangle k's index in the caller's list (null: k)
     const DevMat* sky;       // sky texels when sky mode is on, else null
+    const DevMat* tri_mat;   // rt_triangle.mat per triangle (leaf order with a BVH): RT_SEM_CUDA
+    int cuda;                // rt.h RT_SEM_CUDA (render_kernel_cuda)
+    double cbb[6];           // RT_SEM_CUDA: the triangles' box (lo xyz, hi xyz), hit_BBox
     const double* sph_rinv;  // 1/radius per sphere (sphere_uvmapping's divide)
     int sky_w, sky_h;
     double bvh_srel, bvh_sabs;   // distance-cull slack (rt_bvh.cpp)

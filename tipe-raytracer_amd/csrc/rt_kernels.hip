@@ -205,9 +205,13 @@ __device__ __forceinline__ double dinf() { return __longlong_as_double(0x7ff0000
 // divisions run div_core: a hit needs n >= 1e-4*two_a >> 2^-900, and
 // disc <= 2^760 bounds |n| by 2^512, so every quotient that can decide or
 // become t is exact; smaller n give t < 1e-4 on both paths.
+// CU: main_cuda.cu's hit_sphere (sphere.hu:27-45), t1 >= 0 then t2 >= 0.001;
+// its t1 may be tiny, so the fast division also needs |n| >= 2^-900 there.
+template <bool CU>
 __device__ __forceinline__ bool sphere_exact(double cx, double cy, double cz, double r2, const V3 o, const V3 d,
                                              double two_a, double four_a, bool fast, double rc2a, double& t)
 {
+    const double e1 = CU ? 0.0 : 0.0001, e2 = CU ? 0.001 : 0.0001;
     const double ocx = o.x - cx, ocy = o.y - cy, ocz = o.z - cz;
     const double b = 2.0 * (ocx * d.x + ocy * d.y + ocz * d.z);
     const double c = (ocx * ocx + ocy * ocy + ocz * ocz) - r2;
@@ -219,15 +223,15 @@ __device__ __forceinline__ bool sphere_exact(double cx, double cy, double cz, do
     else sq = sqrt(disc);
     const double n1 = -b - sq;
     if (!(n1 < 0.0)) {
-        if (f) t = div_core(n1, two_a, rc2a);
+        if (f && (!CU || n1 >= 0x1p-900)) t = div_core(n1, two_a, rc2a);
         else t = n1 / two_a;
-        if (t >= 0.0001) return true;
+        if (t >= e1) return true;
     }
     const double n2 = -b + sq;
     if (!(n2 < 0.0)) {
-        if (f) t = div_core(n2, two_a, rc2a);
+        if (f && (!CU || n2 >= 0x1p-900)) t = div_core(n2, two_a, rc2a);
         else t = n2 / two_a;
-        if (t >= 0.0001) return true;
+        if (t >= e2) return true;
     }
     return false;
 }
@@ -242,6 +246,7 @@ __device__ __forceinline__ bool disc_positive(const SphGeo& s, const V3 o, const
 }
 
 // Exact reference scan over every sphere (main.c:59-78 with hit_sphere).
+template <bool CU>
 __device__ __forceinline__ int spheres_exact_scan(const KParams& kp, const V3 o, const V3 d, double two_a,
                                                   double four_a, bool fast, double rc2a, double& t_best)
 {
@@ -250,8 +255,8 @@ __device__ __forceinline__ int spheres_exact_scan(const KParams& kp, const V3 o,
     int win = -1;
     for (int k = 0; k < kp.ns_pad; ++k) {
         double tk;
-        if (sphere_exact(sg[4 * k], sg[4 * k + 1], sg[4 * k + 2], sg[4 * k + 3], o, d, two_a, four_a, fast, rc2a,
-                         tk) &&
+        if (sphere_exact<CU>(sg[4 * k], sg[4 * k + 1], sg[4 * k + 2], sg[4 * k + 3], o, d, two_a, four_a, fast,
+                             rc2a, tk) &&
             tk < t) {
             t = tk;
             win = k;
@@ -283,7 +288,8 @@ __device__ __forceinline__ int spheres_exact_scan(const KParams& kp, const V3 o,
 // Two winners closer than 2M are ambiguous, so a strictly smaller interval is
 // a strictly smaller t_ref (the reference keeps the first of equal t).
 // Non-finite o, d or Hs^2 > 2^1000 make the ray ambiguous up front.
-template <bool COUNT>
+// CU (main_cuda.cu's thresholds): t1 >= 0, t2 >= 0.001, one interval pair each.
+template <bool COUNT, bool CU>
 __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, const V3 d, double a, double two_a,
                                                double four_a, bool fast, double rc2a, double& t_best, Cnt& cnt)
 {
@@ -299,8 +305,10 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     const double Hs2 = Hs * Hs;
     const double T1 = Hs2 * RT_CAND_T1, nT2 = Hs2 * -0x1p-44;
     const double thr = a * 0.0001;
-    const double M = fma(thr, 0x1p-48, Hs * RT_CAND_M);
-    const double thrP = thr + M, thrM = thr - M, M2 = 2.0 * M;
+    const double thr1 = CU ? 0.0 : thr, thr2 = CU ? a * 0.001 : thr;
+    const double M = fma(thr2, 0x1p-48, Hs * RT_CAND_M);
+    const double thrP = thr1 + M, thrM = thr1 - M, M2 = 2.0 * M;
+    const double thrP2 = thr2 + M, thrM2 = thr2 - M;
     double bn = INF;
     int bk = -1;
     // finite o, d, Hs^2 keep every D below finite; anything else takes the exact scan
@@ -324,9 +332,11 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             const double tt = D * r0;
             const double sa = fma(tt * 0.5, fma(-tt, r0, 1.0), tt);
             const double n1 = -h - sa, n2 = sa - h;
-            const double n = n1 >= thrM ? n1 : n2;          // n1 may reach 1e-4: hit_sphere takes t1
-            const bool sure = n >= thrP;
-            amb = amb || (valid && (sure != (n >= thrM)));  // the chosen root straddles 1e-4
+            const bool r1 = n1 >= thrM;                     // n1 may reach 1e-4: hit_sphere takes t1
+            const double n = r1 ? n1 : n2;
+            const double tP = CU ? (r1 ? thrP : thrP2) : thrP, tM = CU ? (r1 ? thrM : thrM2) : thrM;
+            const bool sure = n >= tP;
+            amb = amb || (valid && (sure != (n >= tM)));    // the chosen root straddles 1e-4
             const bool cand = valid && sure;
             const double diff = n - bn;
             const bool closer = cand && diff < -M2;
@@ -341,20 +351,20 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     int win = -1;
     if (!amb && bk >= 0) {
         const SphGeo s = kp.sph[bk];
-        if (sphere_exact(s.cx, s.cy, s.cz, s.r2, o, d, two_a, four_a, fast, rc2a, t)) win = bk;
+        if (sphere_exact<CU>(s.cx, s.cy, s.cz, s.r2, o, d, two_a, four_a, fast, rc2a, t)) win = bk;
         else amb = true;     // cannot happen within the bound; stay exact anyway
 #ifdef RT_DUP_WINNER
         {
             double t2;
-            const bool w2 = sphere_exact(s.cx, s.cy, s.cz, s.r2, v3(launder(o.x), launder(o.y), launder(o.z)), d,
-                                         two_a, four_a, fast, rc2a, t2);
+            const bool w2 = sphere_exact<CU>(s.cx, s.cy, s.cz, s.r2, v3(launder(o.x), launder(o.y), launder(o.z)),
+                                             d, two_a, four_a, fast, rc2a, t2);
             if (opaque_false()) { t = t2; amb = !w2; }
         }
 #endif
     }
     if (amb) {               // exact reference scan for this ray
         if (COUNT) cnt.c[RT_CNT_EXACT_RESCANS] += 1;
-        win = spheres_exact_scan(kp, o, d, two_a, four_a, fast, rc2a, t);
+        win = spheres_exact_scan<CU>(kp, o, d, two_a, four_a, fast, rc2a, t);
     }
     t_best = t;
     return win;
@@ -366,10 +376,11 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
 // the caller's order (BVH leaf order), an equal dst replaces a triangle
 // winner with a larger caller index (orig).  det >= 1e-6 >= 2^-400 puts
 // 1/det on the exact fast division (div_core).
-template <bool COUNT>
+template <bool COUNT, bool CU = false>
 __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, const V3 d, double& best, int& kind,
                                          int& win, int& win_orig)
 {
+    const double eps = CU ? 0.00001 : 0.0000001;     // triangle.hu:262 / mesh.h:88
     const TriGeo g = kp.tri[k];
     const double det = -(d.x * g.nx + d.y * g.ny + d.z * g.nz);
     if (det >= 1E-6) {
@@ -379,13 +390,13 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
         if (det <= 0x1p400) invDet = div_core(1.0, det, rcp_refined(det));
         else invDet = 1 / det;
         const double dst = (ao.x * g.nx + ao.y * g.ny + ao.z * g.nz) * invDet;
-        if (dst >= 0.0000001 && dst <= best) {
+        if (dst >= eps && dst <= best) {
             const int orig = kp.tri_orig ? kp.tri_orig[k] : k;
             if (dst < best || (kind == HIT_TRI && orig < win_orig)) {
                 const double u = (g.acx * dao.x + g.acy * dao.y + g.acz * dao.z) * invDet;
                 const double v = -(g.abx * dao.x + g.aby * dao.y + g.abz * dao.z) * invDet;
                 const double w = 1 - u - v;
-                if (u >= 0.0000001 && v >= 0.0000001 && w >= 0.0000001) {
+                if (u >= eps && v >= eps && w >= eps) {
                     best = dst;
                     kind = HIT_TRI;
                     win = k;
@@ -406,7 +417,7 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
 // behind the origin (tmax < -sabs), or enters it beyond best*(1+srel)+sabs.
 // Slab reciprocals use |d_i| >= 2^-200, which keeps the products finite
 // without changing any decision for unit-length directions.
-template <bool COUNT>
+template <bool COUNT, bool CU>
 __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3 d, double& best, int& kind,
                                          int& win, int& win_orig, Cnt& cnt)
 {
@@ -473,12 +484,12 @@ __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3
                 kend = k + nd->count[c];
                 if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)(kend - k);
             }
-            tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
+            tri_test<COUNT, CU>(kp, k, o, d, best, kind, win, win_orig);
 #ifdef RT_DUP_TRILEAF
             {
                 double b2 = best;
                 int k2 = kind, w2 = win, o2 = win_orig;
-                tri_test<COUNT>(kp, k, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2);
+                tri_test<COUNT, CU>(kp, k, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2);
                 if (opaque_false()) { best = b2; kind = k2; win = w2; win_orig = o2; }
             }
 #endif
@@ -496,7 +507,19 @@ __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3
 
 // closest_hit, main.c:52-92: spheres, then triangles; a strictly closer hit
 // replaces the record.  Returns the winner (kind, index, t).
-template <bool COUNT, bool BVH>
+// hit_BBox, triangle.hu:42-59 (CU mode): IEEE divisions, CUDA's double
+// min/max = fmin/fmax; the triangles are skipped when it fails.
+__device__ __forceinline__ bool cuda_bbox(const KParams& kp, const V3 o, const V3 d)
+{
+    const double t1x = (kp.cbb[0] - o.x) / d.x, t2x = (kp.cbb[3] - o.x) / d.x;
+    const double t1y = (kp.cbb[1] - o.y) / d.y, t2y = (kp.cbb[4] - o.y) / d.y;
+    const double t1z = (kp.cbb[2] - o.z) / d.z, t2z = (kp.cbb[5] - o.z) / d.z;
+    const double tmax = fmin(fmin(fmax(t1x, t2x), fmax(t1y, t2y)), fmax(t1z, t2z));
+    const double tmin = fmax(fmax(fmin(t1x, t2x), fmin(t1y, t2y)), fmin(t1z, t2z));
+    return tmax - tmin > 0;
+}
+
+template <bool COUNT, bool BVH, bool CU = false>
 __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const V3 d, double& t_best, int& idx,
                                            Cnt& cnt)
 {
@@ -511,12 +534,12 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
         cnt.c[RT_CNT_TRI_TESTS] += (unsigned long long)kp.nt;
     }
     double best;
-    int win = spheres_closest<COUNT>(kp, o, d, a, two_a, four_a, fast, rc2a, best, cnt);
+    int win = spheres_closest<COUNT, CU>(kp, o, d, a, two_a, four_a, fast, rc2a, best, cnt);
 #ifdef RT_DUP_SPHERES
     {
         double b2;
-        const int w2 = spheres_closest<COUNT>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, a, two_a,
-                                              four_a, fast, rc2a, b2, cnt);
+        const int w2 = spheres_closest<COUNT, CU>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, a, two_a,
+                                                  four_a, fast, rc2a, b2, cnt);
         const bool f = opaque_false();
         best = f ? b2 : best;
         win = f ? w2 : win;
@@ -524,13 +547,15 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
 #endif
     int kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
     int win_orig = 0;
-    if (BVH) {
-        tris_bvh<COUNT>(kp, o, d, best, kind, win, win_orig, cnt);
+    if (CU && kp.nt > 0 && !cuda_bbox(kp, o, d)) {
+        // main_cuda.cu:40-45: the ray misses the mesh box, no triangle tested
+    } else if (BVH) {
+        tris_bvh<COUNT, CU>(kp, o, d, best, kind, win, win_orig, cnt);
 #ifdef RT_DUP_TRIS
         {
             double b2 = best;
             int k2 = kind, w2 = win, o2 = win_orig;
-            tris_bvh<COUNT>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2, cnt);
+            tris_bvh<COUNT, CU>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2, cnt);
             const bool f = opaque_false();
             best = f ? b2 : best;
             kind = f ? k2 : kind;
@@ -538,7 +563,7 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
         }
 #endif
     } else {
-        for (int k = 0; k < kp.nt; ++k) tri_test<COUNT>(kp, k, o, d, best, kind, win, win_orig);
+        for (int k = 0; k < kp.nt; ++k) tri_test<COUNT, CU>(kp, k, o, d, best, kind, win, win_orig);
     }
     t_best = best;
     idx = win;
@@ -677,6 +702,8 @@ __device__ __forceinline__ double hue_to_rgb(double t1, double t2, double hue)
     if (3.0 * hue < 2.0) return t1 + (t2 - t1) * (KCV(kcb(), KC_TWO_THIRDS) - hue) * 6.0;
     return t1;
 }
+// CU: main_cuda.cu:92-93 raise L and S by 1.20 (main.c:156-157: x1.0)
+template <bool CU = false>
 __device__ __forceinline__ V3 hsl_roundtrip(V3 rgb)
 {
     const double r = rgb.x, g = rgb.y, b = rgb.z;
@@ -694,8 +721,8 @@ __device__ __forceinline__ V3 hsl_roundtrip(V3 rgb)
         else if (mx == b) h = (r - g) / d + 4.0;
         h /= 6.0;
     }
-    l *= 1.0;
-    s *= 1.0;
+    l *= CU ? 1.20 : 1.0;
+    s *= CU ? 1.20 : 1.0;
     if (s == 0.0) return v3(l, l, l);
     const double t2 = (l < 0.5) ? (l * (1.0 + s)) : (l + s - l * s);
     const double t1 = 2.0 * l - t2;
@@ -704,7 +731,7 @@ __device__ __forceinline__ V3 hsl_roundtrip(V3 rgb)
 }
 
 // ambient_occlusion, main.c:94-116: one cast, only distance/dst matters.
-template <bool COUNT, bool BVH>
+template <bool COUNT, bool BVH, bool CU = false>
 __device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const V3 n, double AO, Stream& st,
                                             Cnt& cnt)
 {
@@ -712,7 +739,7 @@ __device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const
     const V3 dir = normalize(n + rd);
     double t;
     int idx;
-    const int kind = closest_hit<COUNT, BVH>(kp, p, dir, t, idx, cnt);
+    const int kind = closest_hit<COUNT, BVH, CU>(kp, p, dir, t, idx, cnt);
     double occ = 0.0;
     if (kind != HIT_NONE) {
         const V3 hp = p + muls(dir, t);
@@ -840,6 +867,76 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, Stream& st,
     acc_add(acc, ACC_RAD, ps.inc());
 }
 
+// tracer, main_cuda.cu:86-141 (rt.h RT_SEM_CUDA).  A pre-pass cast returns
+// emitters (HSL round trip, L and S x1.20) and misses (zeros); the bounce
+// loop starts again from the same ray, so its first cast reuses the pre-pass
+// hit (the COUNT build recasts it, to count what main_cuda.cu casts); no
+// alpha holes, refraction, textures or x1.3 brightening; a triangle's
+// material is its own (kp.tri_mat); albedo/normal are the pre-pass hit's.
+template <bool COUNT, bool BVH>
+__device__ __forceinline__ bool cuda_hit(const KParams& kp, const V3 o, const V3 d, V3& hp, V3& hn, Mat& mat,
+                                         Cnt& cnt)
+{
+    double t;
+    int idx;
+    const int kind = closest_hit<COUNT, BVH, true>(kp, o, d, t, idx, cnt);
+    if (kind == HIT_NONE) return false;
+    hp = o + muls(d, t);                                 // ray_at
+    if (kind == HIT_SPHERE) {
+        const SphGeo s = kp.sph[idx];
+        hn = normalize(hp - v3(s.cx, s.cy, s.cz));       // sphere.hu:31,40
+        mat = load_mat(kp.sph_mat + idx);
+    } else {
+        const TriGeo g = kp.tri[idx];
+        hn = normalize(v3(g.nx, g.ny, g.nz));            // triangle.hu:266
+        mat = load_mat(kp.tri_mat + idx);
+    }
+    return true;
+}
+
+template <bool COUNT, bool BVH>
+__device__ __forceinline__ void trace_cuda(const KParams& kp, V3 o, V3 d, Stream& st, double* acc, Cnt& cnt)
+{
+    V3 hp, hn;
+    Mat mat;
+    if (!cuda_hit<COUNT, BVH>(kp, o, d, hp, hn, mat, cnt)) {    // return BLACK
+        acc_add(acc, ACC_RAD, v3(0, 0, 0));
+        acc_add(acc, ACC_ALB, v3(0, 0, 0));
+        acc_add(acc, ACC_NRM, v3(0, 0, 0));
+        return;
+    }
+    if (mat.es > 0) {
+        const V3 col = hsl_roundtrip<true>(mat.emis);
+        acc_add(acc, ACC_RAD, col);
+        acc_add(acc, ACC_ALB, col);
+        acc_add(acc, ACC_NRM, hn);
+        return;
+    }
+    acc_add(acc, ACC_ALB, mat.diff);                     // the outer hitInfo, main_cuda.cu:140
+    acc_add(acc, ACC_NRM, hn);
+    V3 inc = v3(0, 0, 0), rc = v3(1, 1, 1);
+    for (int i = 0; i < kp.B; i++) {
+        if ((i > 0 || COUNT) && !cuda_hit<COUNT, BVH>(kp, o, d, hp, hn, mat, cnt)) break;
+        o = hp;
+        const V3 diffuse_dir = normalize(hn + random_dir<COUNT>(st, cnt));
+        const V3 reflected_dir = d - muls(hn, 2 * dot(d, hn));
+        d = diffuse_dir + muls(reflected_dir - diffuse_dir, mat.rs);   // vec3_lerp, rtutility.hu:31-35
+        if (kp.useAO) {
+            const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
+            const V3 em = muls(mat.emis, mat.es * 1.5 * AO);
+            inc = inc + mulv(em, rc);
+            rc = mulv(mat.diff, rc);
+            const double occ = ao_factor<COUNT, BVH, true>(kp, hp, hn, AO, st, cnt);
+            rc = mulv(rc, v3(occ, occ, occ));
+        } else {
+            const V3 em = muls(mat.emis, mat.es);
+            inc = inc + mulv(em, rc);
+            rc = mulv(mat.diff, rc);
+        }
+    }
+    acc_add(acc, ACC_RAD, inc);
+}
+
 // write_color_canva, rtutility.h:56-71 (sqrtf of the float-rounded product)
 __device__ __forceinline__ double resolve(double sum, double rapport)
 {
@@ -865,9 +962,10 @@ __device__ __forceinline__ void write_pixel(const KParams& kp, long long li, V3 
     if (kp.radiance) store3(kp.radiance, li, divs(srad, S));
 }
 
-// fill_canva, main.c:245-284: thread = (pixel, chunk of its samples).
-template <bool COUNT, bool BVH, bool SKY>
-__global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIMD) void render_kernel(const KParams kp)
+// Body of render_kernel (main.c semantics) and render_kernel_cuda
+// (main_cuda.cu's): one thread = (pixel, chunk of its samples).
+template <bool COUNT, bool BVH, bool SKY, bool CU>
+__device__ __forceinline__ void render_body(const KParams& kp)
 {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
@@ -905,8 +1003,9 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
             const double jy = -0.5 + 1.0 * unit31(st.next31());
             const int b = opq0();
             const cdptr U = (cdptr)kp.uni;
-            const double u = ((double)x + ju) / U[b + U_WM1];
-            const double v = ((double)g + jv) / U[b + U_HM1];
+            // main.c:265-266; main_cuda.cu:152-153 adds 0.5 first
+            const double u = (CU ? (double)x + 0.5 + ju : (double)x + ju) / U[b + U_WM1];
+            const double v = (CU ? (double)g + 0.5 + jv : (double)g + jv) / U[b + U_HM1];
             const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
             // get_ray, camera.h:42-55
             const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
@@ -917,7 +1016,8 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
             const V3 dest = co + muls(dir, U[b + U_FOCUS]);
             const V3 no = co + v3(dx, dy, 0);
             const V3 rd = normalize(dest - no);
-            trace<COUNT, BVH, SKY>(kp, no, rd, st, acc, cnt);
+            if (CU) trace_cuda<COUNT, BVH>(kp, no, rd, st, acc, cnt);
+            else trace<COUNT, BVH, SKY>(kp, no, rd, st, acc, cnt);
             if (COUNT) {
                 cnt.c[RT_CNT_SAMPLES] += 1;
                 cnt.c[RT_CNT_RNG_DRAWS] += st.n;
@@ -948,6 +1048,21 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
             if (lane == 0 && v) atomicAdd(kp.counters + k, v);
         }
     }
+}
+
+// fill_canva, main.c:245-284: thread = (pixel, chunk of its samples).
+template <bool COUNT, bool BVH, bool SKY>
+__global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIMD) void render_kernel(const KParams kp)
+{
+    render_body<COUNT, BVH, SKY, false>(kp);
+}
+
+// render_canva, main_cuda.cu:143-171 semantics (rt.h RT_SEM_CUDA).
+template <bool COUNT, bool BVH>
+__global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIMD) void render_kernel_cuda(
+    const KParams kp)
+{
+    render_body<COUNT, BVH, false, true>(kp);
 }
 
 // Sum the chunk partials of each pixel in chunk order, then resolve.
@@ -1129,7 +1244,9 @@ static void launch_variant(const KParams& kp, void* stream)
 {
     const dim3 g = grid_for(kp);
     const hipStream_t st = (hipStream_t)stream;
-    if (kp.bvh && kp.sky) hipLaunchKernelGGL((render_kernel<COUNT, true, true>), g, dim3(256), 0, st, kp);
+    if (kp.cuda && kp.bvh) hipLaunchKernelGGL((render_kernel_cuda<COUNT, true>), g, dim3(256), 0, st, kp);
+    else if (kp.cuda) hipLaunchKernelGGL((render_kernel_cuda<COUNT, false>), g, dim3(256), 0, st, kp);
+    else if (kp.bvh && kp.sky) hipLaunchKernelGGL((render_kernel<COUNT, true, true>), g, dim3(256), 0, st, kp);
     else if (kp.bvh) hipLaunchKernelGGL((render_kernel<COUNT, true, false>), g, dim3(256), 0, st, kp);
     else if (kp.sky) hipLaunchKernelGGL((render_kernel<COUNT, false, true>), g, dim3(256), 0, st, kp);
     else hipLaunchKernelGGL((render_kernel<COUNT, false, false>), g, dim3(256), 0, st, kp);

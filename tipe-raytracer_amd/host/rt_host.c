@@ -64,6 +64,21 @@ void rt_host_move_mesh(double x, double y, double z, rt_triangle* t, int n)
 
 void rt_host_free(void* p) { free(p); }
 
+void rt_host_cuda_materials(rt_mesh* m)
+{
+    if (!m || !m->triangles || !m->quelMatPourTri) return;
+    for (int i = 0; i < m->nbTriangles; i++) {
+        const int k = m->quelMatPourTri[i];
+        rt_material* mt = &m->triangles[i].mat;
+        memset(mt, 0, sizeof *mt);
+        if (k < 0 || k >= m->nbMaterials) continue;
+        for (int a = 0; a < 3; a++) mt->diffuseColor.e[a] = (double)(float)(m->kd ? m->kd[k].e[a] : 0.0);
+        const float shininess = (float)(m->ns ? m->ns[k] : 0.0);
+        mt->reflectionStrength = (double)(shininess / 100);     /* triangle.hu:104 */
+        mt->alpha = 1.0;
+    }
+}
+
 /* ---- growable arrays ----------------------------------------------------- */
 typedef struct { void* p; size_t n, cap, sz; } vec_t;
 static int vpush(vec_t* v, const void* x)

@@ -132,3 +132,13 @@ def pyramid_mesh():
 def tree_mesh():
     """C4 mesh: 1tree_tri.obj (1320 tris) at TREE_MOVE."""
     return moved(load_tree_fixture(), TREE_MOVE)
+
+
+def with_cuda_materials(mesh):
+    """rt.h RT_SEM_CUDA: each triangle's own material = the first texel of
+    its material (the Kd-flat texel of a Kd-only MTL, as main_cuda.cu's
+    per-mesh {Kd, black, 0, Ns/100}), in place."""
+    tris, qm, mats, tw, th, nm = mesh
+    for k in range(len(tris)):
+        tris[k].mat = mats[qm[k] * tw * th]
+    return mesh
