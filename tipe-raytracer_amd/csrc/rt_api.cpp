@@ -650,8 +650,9 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, i
     const int W = params->largeur_image;
     const int nrows = row_hi - row_lo + 1;
     const int ndev = (int)devs.size();
-    // One device: one band.  Several: cyclic 8-row tiles (load balance).
-    const int k = ndev == 1 ? nrows : 8;
+    // One device: one band.  Several: cyclic 2-row tiles (load balance: the
+    // busiest device renders at most one tile more than the average).
+    const int k = ndev == 1 ? nrows : 2;
     const int ntiles = (nrows + k - 1) / k;
 
     struct Slot {
