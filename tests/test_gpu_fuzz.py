@@ -75,3 +75,14 @@ def random_scene(seed):
 def test_random_scene_bitexact(seed):
     bundle, p = random_scene(seed)
     check_parity(bundle, p)
+
+
+@pytest.mark.parametrize("seed", range(100, 124))
+def test_random_scene_cuda_semantics_bitexact(seed):
+    """rt.h RT_SEM_CUDA on random scenes: each triangle takes its first texel
+    as its own material (scenes.with_cuda_materials), sky off."""
+    bundle, p = random_scene(seed)
+    if bundle.mesh is not None:
+        scenes.with_cuda_materials(bundle.mesh)
+    p.semantics = tipe_rt.types.RT_SEM_CUDA
+    check_parity(bundle, p)
