@@ -277,6 +277,14 @@ int rt_selftest_math(int op, const double* in, double* out, int n);
  * device 0. */
 int rt_verify_sampler_phi(unsigned long long r0, unsigned long long n, unsigned long long counts[2]);
 
+/* Stress check of the sphere candidate pass (closest_hit's sphere half,
+ * main.c:59-78): for n rays (origin xyz, direction xyz: 6 doubles each) the
+ * candidate pass with its exact fallback against the plain exact scan of
+ * hit_sphere.  counts[0] = rays sent to the exact fallback, counts[1] = rays
+ * whose winner or distance differs (0 is the correctness bar).  Synchronous,
+ * device 0. */
+int rt_verify_sphere_pass(const rt_scene* scene, const double* rays, long long n, unsigned long long counts[2]);
+
 #ifdef __cplusplus
 }
 #endif

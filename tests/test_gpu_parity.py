@@ -285,6 +285,52 @@ def adversarial_sphere_scene():
     return helpers.cornell(extra)
 
 
+def _stress_rays(spheres, n, seed):
+    """Rays that stress the candidate pass's bound: origins on sphere surfaces
+    (as a bounce leaves them), directions near tangent at 1e-3..1e-12, rays
+    aimed at silhouettes (disc ~ 0), unnormalised directions, far origins."""
+    rng = np.random.default_rng(seed)
+    C_ = np.array([[s.center.e[0], s.center.e[1], s.center.e[2]] for s in spheres])
+    R_ = np.array([s.radius for s in spheres])
+
+    def unit(v):
+        return v / np.linalg.norm(v, axis=-1, keepdims=True)
+    m = n // 5
+    k = rng.integers(0, len(R_), m)
+    # 1. surface origins, random and near-tangent directions
+    nrm = unit(rng.normal(size=(m, 3)))
+    o1 = C_[k] + R_[k, None] * nrm
+    tan = unit(np.cross(nrm, rng.normal(size=(m, 3))))
+    eps = rng.choice([0.0, 1e-3, 1e-6, 1e-9, 1e-12], m)[:, None] * rng.choice([-1.0, 1.0], (m, 1))
+    d1 = np.where(rng.random((m, 1)) < 0.5, unit(rng.normal(size=(m, 3))), tan + eps * nrm)
+    # 2. silhouette rays from random box points
+    o2 = rng.uniform([-1, -1, -4], [1, 1, 0.5], (m, 3))
+    k2 = rng.integers(0, len(R_), m)
+    w = C_[k2] - o2
+    perp = unit(np.cross(w, rng.normal(size=(m, 3))))
+    d2 = (C_[k2] + R_[k2, None] * perp * (1 + rng.choice([0, 1e-9, -1e-9, 1e-14], m)[:, None])) - o2
+    # 3. random rays, 4. unnormalised, 5. far origins
+    o3 = rng.uniform([-1, -1, -4], [1, 1, 0.5], (m, 3))
+    d3 = unit(rng.normal(size=(m, 3)))
+    d4 = unit(rng.normal(size=(m, 3))) * 10.0 ** rng.uniform(-3, 3, (m, 1))
+    o5 = unit(rng.normal(size=(m, 3))) * rng.uniform(10, 2000, (m, 1))
+    d5 = unit(rng.uniform(-1, 1, (m, 3)) - o5)
+    o = np.concatenate([o1, o2, o3, o3, o5])
+    d = np.concatenate([d1, d2, d3, d4, d5])
+    return np.concatenate([o, d], axis=1)
+
+
+@pytest.mark.parametrize("which", ["cornell", "adversarial"])
+def test_sphere_candidate_pass_stress(which):
+    """5M stress rays: the candidate pass (with its exact fallback) returns the
+    exact scan's winner and distance bit for bit on every ray."""
+    bundle = helpers.cornell() if which == "cornell" else adversarial_sphere_scene()
+    rays = _stress_rays(bundle.spheres, 5_000_000, 7 if which == "cornell" else 8)
+    fb, bad = tipe_rt.verify_sphere_pass(bundle.scene, rays)
+    assert bad == 0
+    assert fb < len(rays) // 2
+
+
 def test_sphere_candidate_pass_adversarial():
     import torch
     bundle = adversarial_sphere_scene()

@@ -843,6 +843,45 @@ int rt_selftest_math(int op, const double* in, double* out, int n)
     return RT_OK;
 }
 
+int rt_verify_sphere_pass(const rt_scene* scene, const double* rays, long long n, unsigned long long counts[2])
+{
+    if (!counts || !rays || n < 0) return fail(RT_EINVAL, "bad verify arguments");
+    counts[0] = counts[1] = 0;
+    if (n == 0) return RT_OK;
+    int dev = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        int rc = ensure_init_locked();
+        if (rc) return rc;
+        dev = g_devices[0];
+    }
+    rt_device_scene* ds = nullptr;
+    int rc = rt_scene_upload(dev, scene, &ds);
+    if (rc) return rc;
+    DeviceGuard guard(dev);
+    KParams kp;
+    std::memset(&kp, 0, sizeof kp);
+    kp.sph = ds->sph;
+    kp.sph_cand = ds->sph_cand;
+    kp.cand_lmax = ds->cand_lmax;
+    kp.ns = ds->ns;
+    kp.ns_pad = ds->ns_pad;
+    double* d_rays = nullptr;
+    unsigned long long* d = nullptr;
+    hipError_t e = hipMalloc((void**)&d_rays, (size_t)n * 6 * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void**)&d, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemcpy(d_rays, rays, (size_t)n * 6 * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(d, 0, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = (hipError_t)launch_verify_spheres(kp, d_rays, n, d);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(counts, d, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    (void)hipFree(d_rays);
+    (void)hipFree(d);
+    rt_scene_release(ds);
+    if (e != hipSuccess) return fail(RT_EDEVICE, "verify_sphere_pass: %s", hipGetErrorString(e));
+    return RT_OK;
+}
+
 int rt_verify_sampler_phi(unsigned long long r0, unsigned long long n, unsigned long long counts[2])
 {
     if (!counts || r0 > (1ull << 31) || n > (1ull << 31) - r0) return fail(RT_EINVAL, "bad verify range");

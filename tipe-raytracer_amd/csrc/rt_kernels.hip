@@ -1304,6 +1304,44 @@ __global__ __launch_bounds__(256) void verify_phi_kernel(unsigned long long r0, 
     }
 }
 
+// Sphere closest hit of arbitrary rays (o, d: 6 doubles each): the candidate
+// pass (spheres_closest, with its own exact fallback) against the plain exact
+// scan.  counts[0] += rays the candidate pass sent to the exact scan,
+// counts[1] += rays whose winner or t differs (must stay 0).
+__global__ __launch_bounds__(256) void verify_spheres_kernel(const KParams kp, const double* __restrict__ rays,
+                                                            long long n, unsigned long long* counts)
+{
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    bool fb = false, bad = false;
+    if (i < n) {
+        const V3 o = v3(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+        const V3 d = v3(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+        const double a = dot(d, d), two_a = 2 * a, four_a = 4 * a;
+        const bool fast = two_a >= 0x1p-100 && two_a <= 0x1p100;
+        const double rc2a = rcp_refined(two_a);
+        Cnt cnt;
+        cnt.c[RT_CNT_EXACT_RESCANS] = 0;
+        double t1, t2;
+        const int w1 = spheres_closest<true, false>(kp, o, d, a, two_a, four_a, fast, rc2a, t1, cnt);
+        const int w2 = spheres_exact_scan<false>(kp, o, d, two_a, four_a, fast, rc2a, t2);
+        fb = cnt.c[RT_CNT_EXACT_RESCANS] != 0;
+        bad = w1 != w2 || (w1 >= 0 && __double_as_longlong(t1) != __double_as_longlong(t2));
+    }
+    const unsigned long long nf = __popcll(__ballot(fb)), nb = __popcll(__ballot(bad));
+    if ((threadIdx.x & 63) == 0) {
+        if (nf) atomicAdd(counts, nf);
+        if (nb) atomicAdd(counts + 1, nb);
+    }
+}
+
+int launch_verify_spheres(const KParams& kp, const double* d_rays, long long n, unsigned long long* d_counts)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(verify_spheres_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr, kp, d_rays,
+                       n, d_counts);
+    return hipGetLastError();
+}
+
 int launch_verify_phi(unsigned long long r0, unsigned long long n, unsigned long long* d_counts)
 {
     if (n == 0) return hipSuccess;

@@ -59,6 +59,7 @@ def lib():
                                         C.c_void_p, C.c_void_p]
         L.rt_selftest_math.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         L.rt_verify_sampler_phi.argtypes = [C.c_ulonglong, C.c_ulonglong, C.c_void_p]
+        L.rt_verify_sphere_pass.argtypes = [P(Scene), C.c_void_p, C.c_longlong, C.c_void_p]
         L.rt_accumulate_async.argtypes = [C.c_void_p, P(Params), C.c_longlong, P(Tiling), C.c_void_p, C.c_void_p]
         L.rt_resolve_async.argtypes = [C.c_void_p, P(Params), C.c_int, P(Tiling), P(Frame), C.c_void_p]
         L.rt_set_denoise_hook.argtypes = [DENOISE_FN]
@@ -74,7 +75,8 @@ EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error",
                     "rt_device_count", "rt_render_rows", "rt_fill_canva", "rt_scene_upload",
                     "rt_scene_release", "rt_render_async", "rt_assemble_async", "rt_count_async",
                     "rt_selftest_math", "rt_accumulate_async", "rt_resolve_async", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
-                    "rt_denoise_unpack", "rt_denoise_pack_async", "rt_verify_sampler_phi"]
+                    "rt_denoise_unpack", "rt_denoise_pack_async", "rt_verify_sampler_phi",
+                    "rt_verify_sphere_pass"]
 
 # rt_denoise_fn (rt.h): denoiser()'s signature, denoiser.h:31
 DENOISE_FN = C.CFUNCTYPE(None, C.c_int, C.c_int, C.c_void_p, Camera, C.c_void_p, C.c_void_p)
@@ -253,6 +255,14 @@ def verify_sampler_phi(r0=0, n=1 << 31):
     """(fallbacks, mismatches) of the fast phi path over rand() values [r0, r0 + n)."""
     out = (C.c_ulonglong * 2)()
     check(lib().rt_verify_sampler_phi(r0, n, out))
+    return int(out[0]), int(out[1])
+
+
+def verify_sphere_pass(scene, rays):
+    """(fallbacks, mismatches) of the sphere candidate pass on rays (n, 6) float64."""
+    r = np.ascontiguousarray(rays, dtype=np.float64)
+    out = (C.c_ulonglong * 2)()
+    check(lib().rt_verify_sphere_pass(C.byref(scene), r.ctypes.data, len(r), out))
     return int(out[0]), int(out[1])
 
 
