@@ -60,6 +60,12 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
+#ifndef RT_BVH_SM                   // BVH kernel: resumable trace, node visits per round (0: off)
+#define RT_BVH_SM 4
+#endif
+#ifndef RT_BVH_SM_FILL              // ... and the share of lanes (eighths) that must wait to shade
+#define RT_BVH_SM_FILL 6
+#endif
 #ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
 #define RT_WAVES_PER_SIMD_BVH 3
 #endif
@@ -417,91 +423,113 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
 // behind the origin (tmax < -sabs), or enters it beyond best*(1+srel)+sabs.
 // Slab reciprocals use |d_i| >= 2^-200, which keeps the products finite
 // without changing any decision for unit-length directions.
+// The per-lane stack: one LDS allocation per kernel ([kStack4][256]).
+__device__ __forceinline__ unsigned short* bvh_stack()
+{
+    __shared__ unsigned short stk_lds[kStack4 * 256];
+    return stk_lds + threadIdx.x;
+}
+__device__ __forceinline__ V3 bvh_inv(const V3 d)
+{
+    const double lim = 0x1p-200;
+    return v3(1.0 / (fabs(d.x) < lim ? copysign(lim, d.x) : d.x),
+              1.0 / (fabs(d.y) < lim ? copysign(lim, d.y) : d.y),
+              1.0 / (fabs(d.z) < lim ? copysign(lim, d.z) : d.z));
+}
+
+// One node visit: the four child boxes, the triangles of the hit leaves, then
+// the next node (nearest hit internal child, else the stack top).  Returns
+// false when the traversal is over.  tris_bvh loops it to the end; the
+// resumable trace (render_sm) runs a bounded number of visits per round.
+template <bool COUNT, bool CU>
+__device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3 d, const V3 inv,
+                                         unsigned short* stk, int& node, int& sp, double& best, int& kind,
+                                         int& win, int& win_orig, Cnt& cnt)
+{
+    const double srel = 1.0 + kp.bvh_srel, sabs = kp.bvh_sabs;
+    const BvhNode4* nd = kp.bvh + node;
+    if (COUNT) {
+        cnt.c[RT_CNT_BVH_NODES] += 1;
+        // one lane per wave step adds 64 lane slots
+        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1)
+            cnt.c[RT_CNT_BVH_LANE_SLOTS] += 64;
+    }
+    bool h[4];
+    double tn[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const double x0 = ((double)nd->lo[0][c] - o.x) * inv.x, x1 = ((double)nd->hi[0][c] - o.x) * inv.x;
+        const double y0 = ((double)nd->lo[1][c] - o.y) * inv.y, y1 = ((double)nd->hi[1][c] - o.y) * inv.y;
+        const double z0 = ((double)nd->lo[2][c] - o.z) * inv.z, z1 = ((double)nd->hi[2][c] - o.z) * inv.z;
+        const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
+        const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
+        h[c] = nd->count[c] >= 0 && tmin <= tmax && tmax >= -sabs && tmin <= best * srel + sabs;
+        tn[c] = tmin;
+    }
+    int next = -1;
+    double tnext = 0.0;
+    unsigned lm = 0;                                     // hit leaf slots
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (!h[c]) continue;
+        const int ch = nd->child[c], n = nd->count[c];
+        if (n > 0) {
+            lm |= 1u << c;
+        } else if (next < 0) {
+            next = ch;
+            tnext = tn[c];
+        } else {
+            int push = ch;
+            if (tn[c] < tnext) {                         // nearer: enter it, push the previous pick
+                push = next;
+                next = ch;
+                tnext = tn[c];
+            }
+            stk[sp * 256] = (unsigned short)push;
+            ++sp;
+        }
+    }
+    // The triangles of every hit leaf in one loop, one triangle per lane and
+    // iteration: the wave runs max-over-lanes iterations instead of one
+    // divergent loop per child slot.
+    int k = 0, kend = 0;
+    while (lm != 0u || k < kend) {
+        if (k >= kend) {
+            const int c = __ffs(lm) - 1;
+            lm &= lm - 1u;
+            k = nd->child[c];
+            kend = k + nd->count[c];
+            if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)(kend - k);
+        }
+        tri_test<COUNT, CU>(kp, k, o, d, best, kind, win, win_orig);
+#ifdef RT_DUP_TRILEAF
+        {
+            double b2 = best;
+            int k2 = kind, w2 = win, o2 = win_orig;
+            tri_test<COUNT, CU>(kp, k, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2);
+            if (opaque_false()) { best = b2; kind = k2; win = w2; win_orig = o2; }
+        }
+#endif
+        ++k;
+    }
+    if (next >= 0) {
+        node = next;
+        return true;
+    }
+    if (sp == 0) return false;
+    --sp;
+    node = stk[sp * 256];
+    return true;
+}
+
 template <bool COUNT, bool CU>
 __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3 d, double& best, int& kind,
                                          int& win, int& win_orig, Cnt& cnt)
 {
-    __shared__ unsigned short stk_lds[kStack4 * 256];
-    unsigned short* stk = stk_lds + threadIdx.x;
-    const double lim = 0x1p-200;
-    const double ix = 1.0 / (fabs(d.x) < lim ? copysign(lim, d.x) : d.x);
-    const double iy = 1.0 / (fabs(d.y) < lim ? copysign(lim, d.y) : d.y);
-    const double iz = 1.0 / (fabs(d.z) < lim ? copysign(lim, d.z) : d.z);
-    const double srel = 1.0 + kp.bvh_srel, sabs = kp.bvh_sabs;
+    unsigned short* stk = bvh_stack();
+    const V3 inv = bvh_inv(d);
     int node = 0, sp = 0;
-    while (true) {
-        const BvhNode4* nd = kp.bvh + node;
-        if (COUNT) {
-            cnt.c[RT_CNT_BVH_NODES] += 1;
-            // one lane per wave step adds 64 lane slots
-            if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1)
-                cnt.c[RT_CNT_BVH_LANE_SLOTS] += 64;
-        }
-        bool h[4];
-        double tn[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const double x0 = ((double)nd->lo[0][c] - o.x) * ix, x1 = ((double)nd->hi[0][c] - o.x) * ix;
-            const double y0 = ((double)nd->lo[1][c] - o.y) * iy, y1 = ((double)nd->hi[1][c] - o.y) * iy;
-            const double z0 = ((double)nd->lo[2][c] - o.z) * iz, z1 = ((double)nd->hi[2][c] - o.z) * iz;
-            const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
-            const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
-            h[c] = nd->count[c] >= 0 && tmin <= tmax && tmax >= -sabs && tmin <= best * srel + sabs;
-            tn[c] = tmin;
-        }
-        int next = -1;
-        double tnext = 0.0;
-        unsigned lm = 0;                                 // hit leaf slots
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (!h[c]) continue;
-            const int ch = nd->child[c], n = nd->count[c];
-            if (n > 0) {
-                lm |= 1u << c;
-            } else if (next < 0) {
-                next = ch;
-                tnext = tn[c];
-            } else {
-                int push = ch;
-                if (tn[c] < tnext) {                     // nearer: enter it, push the previous pick
-                    push = next;
-                    next = ch;
-                    tnext = tn[c];
-                }
-                stk[sp * 256] = (unsigned short)push;
-                ++sp;
-            }
-        }
-        // The triangles of every hit leaf in one loop, one triangle per lane
-        // and iteration: the wave runs max-over-lanes iterations instead of
-        // one divergent loop per child slot.
-        int k = 0, kend = 0;
-        while (lm != 0u || k < kend) {
-            if (k >= kend) {
-                const int c = __ffs(lm) - 1;
-                lm &= lm - 1u;
-                k = nd->child[c];
-                kend = k + nd->count[c];
-                if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)(kend - k);
-            }
-            tri_test<COUNT, CU>(kp, k, o, d, best, kind, win, win_orig);
-#ifdef RT_DUP_TRILEAF
-            {
-                double b2 = best;
-                int k2 = kind, w2 = win, o2 = win_orig;
-                tri_test<COUNT, CU>(kp, k, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2);
-                if (opaque_false()) { best = b2; kind = k2; win = w2; win_orig = o2; }
-            }
-#endif
-            ++k;
-        }
-        if (next >= 0) {
-            node = next;
-        } else {
-            if (sp == 0) break;
-            --sp;
-            node = stk[sp * 256];
-        }
+    while (bvh_step<COUNT, CU>(kp, o, d, inv, stk, node, sp, best, kind, win, win_orig, cnt)) {
     }
 }
 
@@ -519,9 +547,10 @@ __device__ __forceinline__ bool cuda_bbox(const KParams& kp, const V3 o, const V
     return tmax - tmin > 0;
 }
 
-template <bool COUNT, bool BVH, bool CU = false>
-__device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const V3 d, double& t_best, int& idx,
-                                           Cnt& cnt)
+// The sphere half of closest_hit (and the cast counters): the winner index
+// or -1, its t in best (+inf when none).
+template <bool COUNT, bool CU>
+__device__ __forceinline__ int cast_spheres(const KParams& kp, const V3 o, const V3 d, double& best, Cnt& cnt)
 {
     const double a = dot(d, d);          // sphere.h:20 (same for every sphere)
     const double two_a = 2 * a;          // sphere.h:27,36
@@ -533,7 +562,6 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
         cnt.c[RT_CNT_SPHERE_TESTS] += (unsigned long long)kp.ns;
         cnt.c[RT_CNT_TRI_TESTS] += (unsigned long long)kp.nt;
     }
-    double best;
     int win = spheres_closest<COUNT, CU>(kp, o, d, a, two_a, four_a, fast, rc2a, best, cnt);
 #ifdef RT_DUP_SPHERES
     {
@@ -545,6 +573,15 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
         win = f ? w2 : win;
     }
 #endif
+    return win;
+}
+
+template <bool COUNT, bool BVH, bool CU = false>
+__device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const V3 d, double& t_best, int& idx,
+                                           Cnt& cnt)
+{
+    double best;
+    int win = cast_spheres<COUNT, CU>(kp, o, d, best, cnt);
     int kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
     int win_orig = 0;
     if (CU && kp.nt > 0 && !cuda_bbox(kp, o, d)) {
@@ -962,6 +999,282 @@ __device__ __forceinline__ void write_pixel(const KParams& kp, long long li, V3 
     if (kp.radiance) store3(kp.radiance, li, divs(srad, S));
 }
 
+// Primary ray of sample st (main.c:258-270; camera.h:42-55 get_ray).
+template <bool CU>
+__device__ __forceinline__ void camera_ray(const KParams& kp, int x, int g, Stream& st, V3& no, V3& rd)
+{
+    const double ju = -0.5 + 1.0 * unit31(st.next31());     // randomDouble(-0.5, 0.5)
+    const double jv = -0.5 + 1.0 * unit31(st.next31());
+    const double jx = -0.5 + 1.0 * unit31(st.next31());
+    const double jy = -0.5 + 1.0 * unit31(st.next31());
+    const int b = opq0();
+    const cdptr U = (cdptr)kp.uni;
+    // main.c:265-266; main_cuda.cu:152-153 adds 0.5 first
+    const double u = (CU ? (double)x + 0.5 + ju : (double)x + ju) / U[b + U_WM1];
+    const double v = (CU ? (double)g + 0.5 + jv : (double)g + jv) / U[b + U_HM1];
+    const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
+    // get_ray, camera.h:42-55
+    const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
+    const V3 ch = v3(U[b + U_CAM_H], U[b + U_CAM_H + 1], U[b + U_CAM_H + 2]);
+    const V3 cv = v3(U[b + U_CAM_V], U[b + U_CAM_V + 1], U[b + U_CAM_V + 2]);
+    const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
+    const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));
+    const V3 dest = co + muls(dir, U[b + U_FOCUS]);
+    no = co + v3(dx, dy, 0);
+    rd = normalize(dest - no);
+}
+
+// Resumable trace for the BVH kernel: the same tracer and
+// ambient_occlusion arithmetic as trace() + ao_factor(), as a per-lane state
+// machine (LanePath).  A lane in
+//   SM_RESOLVE shades the hit of its finished cast (a bounce or an AO cast),
+//   SM_CAM     starts its next sample (or is done),
+//   SM_CAST    runs the sphere half of the next cast and sets up traversal,
+//   SM_TRAV    visits nodes of the triangle BVH,
+// and a lane's casts, draws and sums happen in the same order as in trace(),
+// so results are bit-identical.  samples_sm runs it (RT_BVH_SM > 0): every
+// round each lane runs its phase, at most RT_BVH_SM node visits; a lane
+// whose traversal is short moves on to its next cast instead of idling until
+// the wave's longest traversal ends.  C4: 357 -> 422 Msamples/s, traversal
+// lane slots 258 -> 97 per sample (RT_BVH_SM 4, RT_BVH_SM_FILL 6).
+enum : int { SM_RESOLVE = 0, SM_CAM = 1, SM_CAST = 2, SM_TRAV = 3, SM_DONE = 4 };
+
+template <bool COUNT, bool SKY>
+struct LanePath {
+    Stream st;
+    V3 o, d, cd;                                 // ray, next bounce direction, current cast's direction
+    V3 inc, rc, inv;
+    double top_n2, best;
+    int i, kind, win, win_orig, node, sp, s, state;
+    bool chain, ao_cast;
+
+    __device__ __forceinline__ void init(int s0, int s1)
+    {
+        o = d = cd = inc = rc = inv = v3(0, 0, 0);
+        top_n2 = 1.0;
+        best = 0.0;
+        i = 0; kind = HIT_NONE; win = -1; win_orig = 0; node = 0; sp = 0;
+        chain = true;
+        ao_cast = false;
+        s = s0;
+        state = s0 < s1 ? SM_CAM : SM_DONE;
+    }
+
+    // tracer's bounce body after the cast (main.c:127-241), or
+    // ambient_occlusion's tail (main.c:104-115) for an AO cast
+    __device__ __forceinline__ void resolve(const KParams& kp, double* acc, Cnt& cnt)
+    {
+        bool more = true;                    // the path goes on to bounce i + 1
+        bool add_inc = true;                 // false: direct view of a light (tracer returns early)
+        st.k0 = kp.key0;                     // the key from the kernel argument (uniform), not
+        st.k1 = kp.key1;                     // a loop-carried copy
+        if (ao_cast) {
+            // ambient_occlusion's tail, main.c:104-115
+            const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
+            double occ = 0.0;
+            if (kind != HIT_NONE) {
+                const V3 hp = o + muls(cd, best);
+                const V3 df = hp - o;
+                const double distance = sqrt(dot(df, df));
+                double att = distance / best;
+                att = pm_pow(att, AO);
+                occ = occ + att;
+            }
+            occ = (occ / 1.0) / AO;
+            rc = mulv(rc, v3(occ, occ, occ));
+            ao_cast = false;
+        } else if (kind == HIT_NONE) {       // miss: the path ends, main.c:236-238
+            if (chain) {
+                acc_add(acc, ACC_ALB, v3(0, 0, 0));
+                acc_add(acc, ACC_NRM, v3(0, 0, 0));
+            }
+            more = false;
+        } else {
+            V3 hp, hn;
+            Mat mat;
+            if (kind == HIT_SPHERE) {
+                const SphGeo sg = kp.sph[win];
+                hp = o + muls(d, best);
+                hn = normalize(hp - v3(sg.cx, sg.cy, sg.cz));
+                mat = load_mat(kp.sph_mat + win);
+                if (SKY && win == kp.ns - 1) sky_material(kp, win, sg, hp, mat);
+            } else {
+                if (COUNT) cnt.c[RT_CNT_TEX_HITS] += 1;
+                const TriGeo tg = kp.tri[win];
+                hp = o + muls(d, best);
+                hn = normalize(v3(tg.nx, tg.ny, tg.nz));
+                mat = tri_material(kp, win, hp, hn);
+            }
+            bool lit = false;
+            if (chain) {
+                if (mat.es > 0) {
+                    const V3 col = hsl_roundtrip(mat.emis);
+                    acc_add(acc, ACC_RAD, col);
+                    acc_add(acc, ACC_ALB, col);
+                    acc_add(acc, ACC_NRM, hn);
+                    lit = true;
+                } else if (!(mat.alpha < 0.0001) || i == kp.B - 1) {
+                    acc_add(acc, ACC_ALB, mat.diff);
+                    acc_add(acc, ACC_NRM, hn);
+                    chain = mat.alpha < 0.0001;
+                }
+            }
+            if (lit) {
+                more = false;
+                add_inc = false;
+            } else {
+                o = hp;
+                const V3 diffuse_dir = normalize(hn + random_dir<COUNT>(st, cnt));
+                const V3 reflected_dir = d - muls(hn, 2 * dot(d, hn));
+                const V3 dr = diffuse_dir + muls(reflected_dir - diffuse_dir, mat.rs);
+                bool shade = !(mat.alpha < 0.0001);  // not an alpha hole (main.c:200-206)
+                if (shade) {
+                    chain = false;
+                    if (mat.alpha <= 0.99) {
+                        if (COUNT) cnt.c[RT_CNT_REFRACT] += 1;
+                        V3 nn = hn;
+                        double n1, n2;
+                        if (dot(d, hn) > 0) {
+                            nn = v3(-hn.x, -hn.y, -hn.z);
+                            n1 = mat.ior;
+                            n2 = top_n2;
+                        } else {
+                            n1 = top_n2;
+                            n2 = mat.ior;
+                            top_n2 = mat.ior;
+                        }
+                        const V3 refr = refracted(d, nn, n1, n2);
+                        const double rnd = 0.0 + 1.0 * unit31(st.next31());
+                        if (rnd > mat.alpha) {
+                            d = refr;
+                            shade = false;
+                        } else {
+                            d = dr;
+                        }
+                    } else {
+                        d = dr;
+                    }
+                }
+                if (shade) {
+                    V3 r = rc;
+                    if (kp.useAO) {
+                        const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
+                        const V3 em = muls(mat.emis, mat.es * 1.5 * AO);
+                        inc = inc + mulv(em, r);
+                        if (r.x > 0.5 || r.y > 0.5 || r.z > 0.5) r = mulv(mat.diff, muls(r, 1.3));
+                        rc = mulv(mat.diff, r);
+                        // ambient_occlusion's cast (main.c:96-103): from hp along n + random
+                        cd = normalize(hn + random_dir<COUNT>(st, cnt));
+                        ao_cast = true;
+                    } else {
+                        const V3 em = muls(mat.emis, mat.es);
+                        inc = inc + mulv(em, r);
+                        if (r.x > 0.5 || r.y > 0.5 || r.z > 0.5) r = mulv(mat.diff, muls(r, 1.3));
+                        rc = mulv(mat.diff, r);
+                    }
+                }
+            }
+        }
+        if (ao_cast) {
+            state = SM_CAST;
+        } else {
+            if (more) {
+                ++i;
+                more = i < kp.B;
+            }
+            if (more) {
+                cd = d;
+                state = SM_CAST;
+            } else {
+                if (add_inc) acc_add(acc, ACC_RAD, inc);
+                if (COUNT) {
+                    cnt.c[RT_CNT_SAMPLES] += 1;
+                    cnt.c[RT_CNT_RNG_DRAWS] += st.n;
+                }
+                ++s;
+                state = SM_CAM;
+            }
+        }
+    }
+
+    // the next sample's primary ray (fill_canva's sample loop, main.c:258-270)
+    __device__ __forceinline__ void start(const KParams& kp, int x, int g, uint32_t pixel, int s1, uint32_t* rng,
+                                          double* acc, Cnt& cnt)
+    {
+        if (s >= s1) {
+            state = SM_DONE;
+        } else {
+            st.start(pixel, (uint32_t)(kp.s_base + s), kp.key0, kp.key1, rng);
+            camera_ray<false>(kp, x, g, st, o, d);
+            cd = d;
+            inc = v3(0, 0, 0);
+            rc = v3(1, 1, 1);
+            top_n2 = 1.0;
+            i = 0;
+            chain = true;
+            ao_cast = false;
+            if (kp.B <= 0) {                 // tracer returns (0, 0, 0) albedo/normal
+                acc_add(acc, ACC_ALB, v3(0, 0, 0));
+                acc_add(acc, ACC_NRM, v3(0, 0, 0));
+                acc_add(acc, ACC_RAD, inc);
+                if (COUNT) {
+                    cnt.c[RT_CNT_SAMPLES] += 1;
+                    cnt.c[RT_CNT_RNG_DRAWS] += st.n;
+                }
+                ++s;
+            } else {
+                state = SM_CAST;
+            }
+        }
+    }
+
+    // closest_hit's sphere half and the traversal set-up
+    __device__ __forceinline__ void cast(const KParams& kp, Cnt& cnt)
+    {
+        win = cast_spheres<COUNT, false>(kp, o, cd, best, cnt);
+        kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
+        win_orig = 0;
+        inv = bvh_inv(cd);
+        node = 0;
+        sp = 0;
+        state = SM_TRAV;
+    }
+
+    // up to k node visits; RESOLVE when the traversal is over
+    __device__ __forceinline__ void trav(const KParams& kp, unsigned short* stk, int k, Cnt& cnt)
+    {
+#pragma unroll 1
+        for (int j = 0; j < k; ++j) {
+            if (!bvh_step<COUNT, false>(kp, o, cd, inv, stk, node, sp, best, kind, win, win_orig, cnt)) {
+                state = SM_RESOLVE;
+                break;
+            }
+        }
+    }
+};
+
+#if RT_BVH_SM > 0
+template <bool COUNT, bool SKY>
+__device__ __forceinline__ void samples_sm(const KParams& kp, int x, int g, uint32_t pixel, int s0, int s1,
+                                           uint32_t* rng, double* acc, Cnt& cnt)
+{
+    unsigned short* stk = bvh_stack();
+    LanePath<COUNT, SKY> L;
+    L.init(s0, s1);
+    while (L.state != SM_DONE) {
+        // shade/start/cast only once enough of the wave waits for it (in
+        // eighths of its live lanes, RT_BVH_SM_FILL); else traverse on
+        const unsigned long long live = __ballot(1), wait = __ballot(L.state != SM_TRAV);
+        const bool go = wait == live || __popcll(wait) * 8 >= __popcll(live) * RT_BVH_SM_FILL;
+        if (go && L.state == SM_RESOLVE) L.resolve(kp, acc, cnt);
+        if (go && L.state == SM_CAM) L.start(kp, x, g, pixel, s1, rng, acc, cnt);
+        if (go && L.state == SM_CAST) L.cast(kp, cnt);
+        if (L.state == SM_TRAV) L.trav(kp, stk, RT_BVH_SM, cnt);
+    }
+}
+#endif
+
+
 // Body of render_kernel (main.c semantics) and render_kernel_cuda
 // (main_cuda.cu's): one thread = (pixel, chunk of its samples).
 template <bool COUNT, bool BVH, bool SKY, bool CU>
@@ -994,28 +1307,16 @@ __device__ __forceinline__ void render_body(const KParams& kp)
         const bool carry = !COUNT && kp.sums && kp.chunks == 1;
 #pragma unroll
         for (int j = 0; j < 9; ++j) acc[j * 256] = carry ? kp.sums[li * 9 + j] : 0.0;
+#if RT_BVH_SM > 0
+        if constexpr (BVH && !CU) {
+            samples_sm<COUNT, SKY>(kp, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc, cnt);
+        } else
+#endif
         for (int s = s0; s < s1; ++s) {
             Stream st;
             st.start(pixel, (uint32_t)(kp.s_base + s), kp.key0, kp.key1, rng_lds + threadIdx.x);
-            const double ju = -0.5 + 1.0 * unit31(st.next31());     // randomDouble(-0.5, 0.5)
-            const double jv = -0.5 + 1.0 * unit31(st.next31());
-            const double jx = -0.5 + 1.0 * unit31(st.next31());
-            const double jy = -0.5 + 1.0 * unit31(st.next31());
-            const int b = opq0();
-            const cdptr U = (cdptr)kp.uni;
-            // main.c:265-266; main_cuda.cu:152-153 adds 0.5 first
-            const double u = (CU ? (double)x + 0.5 + ju : (double)x + ju) / U[b + U_WM1];
-            const double v = (CU ? (double)g + 0.5 + jv : (double)g + jv) / U[b + U_HM1];
-            const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
-            // get_ray, camera.h:42-55
-            const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
-            const V3 ch = v3(U[b + U_CAM_H], U[b + U_CAM_H + 1], U[b + U_CAM_H + 2]);
-            const V3 cv = v3(U[b + U_CAM_V], U[b + U_CAM_V + 1], U[b + U_CAM_V + 2]);
-            const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
-            const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));
-            const V3 dest = co + muls(dir, U[b + U_FOCUS]);
-            const V3 no = co + v3(dx, dy, 0);
-            const V3 rd = normalize(dest - no);
+            V3 no, rd;
+            camera_ray<CU>(kp, x, g, st, no, rd);
             if (CU) trace_cuda<COUNT, BVH>(kp, no, rd, st, acc, cnt);
             else trace<COUNT, BVH, SKY>(kp, no, rd, st, acc, cnt);
             if (COUNT) {
