@@ -212,6 +212,12 @@ enum {
                              reference's brute-force count)              */
     RT_CNT_BVH_LANE_SLOTS, /* 64 x wave-level BVH traversal steps (GPU
                              diagnostic; bvh_nodes / this = SIMD efficiency) */
+    RT_CNT_LEAF_LANE_SLOTS, /* 64 x wave-level iterations of the BVH leaf
+                             loop (GPU diagnostic; vs bvh_tri_tests)     */
+    RT_CNT_CAST_LANE_SLOTS, /* 64 x wave-level sphere passes (GPU
+                             diagnostic; vs casts)                       */
+    RT_CNT_SHADE_LANE_SLOTS, /* 64 x wave-level hit resolutions (bounce
+                             shading or AO tail; GPU diagnostic)         */
     RT_NCOUNTERS
 };
 /* Same traversal as rt_render_async, no frame; adds event counts into the

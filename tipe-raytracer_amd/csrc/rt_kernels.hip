@@ -66,6 +66,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_BVH_SM_FILL              // ... and the share of lanes (eighths) that must wait to shade
 #define RT_BVH_SM_FILL 6
 #endif
+#ifndef RT_BVH_COOP                 // BVH kernel: wave-cooperative deep traversal once this many
+#define RT_BVH_COOP 1               // lanes wait for it (0: off, samples_sm)
+#endif
 #ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
 #define RT_WAVES_PER_SIMD_BVH 3
 #endif
@@ -198,6 +201,12 @@ struct PathState<false> {
 struct Cnt {
     unsigned long long c[RT_NCOUNTERS];
 };
+
+// COUNT diagnostics: one lane per wave-level execution adds 64 lane slots.
+__device__ __forceinline__ void wave_slots(Cnt& cnt, int k)
+{
+    if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1) cnt.c[k] += 64;
+}
 
 enum : int { HIT_NONE = 0, HIT_SPHERE = 1, HIT_TRI = 2 };
 
@@ -450,9 +459,7 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
     const BvhNode4* nd = kp.bvh + node;
     if (COUNT) {
         cnt.c[RT_CNT_BVH_NODES] += 1;
-        // one lane per wave step adds 64 lane slots
-        if ((int)(threadIdx.x & 63) == __ffsll((unsigned long long)__ballot(1)) - 1)
-            cnt.c[RT_CNT_BVH_LANE_SLOTS] += 64;
+        wave_slots(cnt, RT_CNT_BVH_LANE_SLOTS);
     }
     bool h[4];
     double tn[4];
@@ -494,6 +501,7 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
     // divergent loop per child slot.
     int k = 0, kend = 0;
     while (lm != 0u || k < kend) {
+        if (COUNT) wave_slots(cnt, RT_CNT_LEAF_LANE_SLOTS);
         if (k >= kend) {
             const int c = __ffs(lm) - 1;
             lm &= lm - 1u;
@@ -561,6 +569,7 @@ __device__ __forceinline__ int cast_spheres(const KParams& kp, const V3 o, const
         cnt.c[RT_CNT_CASTS] += 1;
         cnt.c[RT_CNT_SPHERE_TESTS] += (unsigned long long)kp.ns;
         cnt.c[RT_CNT_TRI_TESTS] += (unsigned long long)kp.nt;
+        wave_slots(cnt, RT_CNT_CAST_LANE_SLOTS);
     }
     int win = spheres_closest<COUNT, CU>(kp, o, d, a, two_a, four_a, fast, rc2a, best, cnt);
 #ifdef RT_DUP_SPHERES
@@ -815,6 +824,7 @@ __device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, Stream& st,
         double t;
         int idx;
         const int kind = closest_hit<COUNT, BVH>(kp, o, d, t, idx, cnt);
+        if (COUNT) wave_slots(cnt, RT_CNT_SHADE_LANE_SLOTS);
         if (kind == HIT_NONE) {                          // miss: the path ends, main.c:236-238
             if (chain) {                                 // albedo/normal of a missed chain ray: 0
                 acc_add(acc, 3, v3(0, 0, 0));            // (main.c:137-140 reads uninitialised
@@ -1064,6 +1074,7 @@ struct LanePath {
     // ambient_occlusion's tail (main.c:104-115) for an AO cast
     __device__ __forceinline__ void resolve(const KParams& kp, double* acc, Cnt& cnt)
     {
+        if (COUNT) wave_slots(cnt, RT_CNT_SHADE_LANE_SLOTS);
         bool more = true;                    // the path goes on to bounce i + 1
         bool add_inc = true;                 // false: direct view of a light (tracer returns early)
         st.k0 = kp.key0;                     // the key from the kernel argument (uniform), not
@@ -1275,6 +1286,237 @@ __device__ __forceinline__ void samples_sm(const KParams& kp, int x, int g, uint
 #endif
 
 
+#if RT_BVH_COOP > 0
+// Wave-cooperative traversal of the deep casts (RT_BVH_COOP > 0).  About 5 %
+// of C4's casts go below the tree's root; walked by their own lanes they
+// keep a wave at a few active lanes for ~25 node visits and ~12 triangle
+// tests (leaf loop 2.6 % lane efficiency).  Here a lane runs its cast's root
+// node itself; a deeper cast parks (SM_TRAV) and once RT_BVH_COOP lanes of
+// the wave are parked (or nothing else can move) every live lane of the wave
+// works on their subtrees: a task is (ray, node); a lane walks its task
+// depth-first with its own LDS stack and hands siblings to a per-wave LIFO
+// (so idle lanes pick them up) while that holds fewer than 64 entries.  The
+// ray is read from its owner lane (ds_bpermute); triangle hits are merged
+// into the owner's record in a wave-uniform loop with the same rule as
+// tri_test (strictly closer, or an equal-dst triangle with a smaller caller
+// index; a sphere keeps an equal-dst hit).  That rule is a total order, so
+// the winner is the one trace() finds, whatever order the triangles are
+// tested in; culling against an older `best` only tests more boxes.
+__device__ __forceinline__ double rl_d(double v, int l)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double shfl_d(double v, int src)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl((int)b, src, 64), hi = __shfl((int)(b >> 32), src, 64);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ unsigned long long lanes_below() { return (1ull << (threadIdx.x & 63)) - 1ull; }
+
+// Append each lane's n (0..4) items to the wave's LIFO (cnt: wave-uniform).
+__device__ __forceinline__ void lifo_push(volatile unsigned* q, int& cnt, int n, const unsigned* it)
+{
+    unsigned long long b[4];
+    int base = cnt, tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b[j] = __ballot(n > j);
+    int off = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        off += __popcll(b[j] & lanes_below());
+        tot += __popcll(b[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (j < n) q[base + off + j] = it[j];
+    cnt = base + tot;
+    __builtin_amdgcn_wave_barrier();
+}
+
+// One node visit of a cooperative task: as bvh_step, but hit internal
+// children other than the next one go to push[] (for the LIFO) when
+// to_lifo, else on the lane's own stack.  hit: a triangle beat the record.
+template <bool COUNT>
+__device__ __forceinline__ bool coop_step(const KParams& kp, const V3 o, const V3 d, const V3 inv,
+                                          unsigned short* stk, int& node, int& sp, double& best, int& kind,
+                                          int& win, int& win_orig, bool& hit, bool to_lifo, unsigned* push,
+                                          int& npush, Cnt& cnt)
+{
+    const double srel = 1.0 + kp.bvh_srel, sabs = kp.bvh_sabs;
+    const BvhNode4* nd = kp.bvh + node;
+    if (COUNT) {
+        cnt.c[RT_CNT_BVH_NODES] += 1;
+        wave_slots(cnt, RT_CNT_BVH_LANE_SLOTS);
+    }
+    bool h[4];
+    double tn[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const double x0 = ((double)nd->lo[0][c] - o.x) * inv.x, x1 = ((double)nd->hi[0][c] - o.x) * inv.x;
+        const double y0 = ((double)nd->lo[1][c] - o.y) * inv.y, y1 = ((double)nd->hi[1][c] - o.y) * inv.y;
+        const double z0 = ((double)nd->lo[2][c] - o.z) * inv.z, z1 = ((double)nd->hi[2][c] - o.z) * inv.z;
+        const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
+        const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
+        h[c] = nd->count[c] >= 0 && tmin <= tmax && tmax >= -sabs && tmin <= best * srel + sabs;
+        tn[c] = tmin;
+    }
+    int next = -1;
+    double tnext = 0.0;
+    unsigned lm = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (!h[c]) continue;
+        const int ch = nd->child[c], n = nd->count[c];
+        if (n > 0) {
+            lm |= 1u << c;
+        } else if (next < 0) {
+            next = ch;
+            tnext = tn[c];
+        } else {
+            int pu = ch;
+            if (tn[c] < tnext) {
+                pu = next;
+                next = ch;
+                tnext = tn[c];
+            }
+            if (to_lifo) {
+                push[npush] = (unsigned)pu;
+                ++npush;
+            } else {
+                stk[sp * 256] = (unsigned short)pu;
+                ++sp;
+            }
+        }
+    }
+    int k = 0, kend = 0;
+    while (lm != 0u || k < kend) {
+        if (COUNT) wave_slots(cnt, RT_CNT_LEAF_LANE_SLOTS);
+        if (k >= kend) {
+            const int c = __ffs(lm) - 1;
+            lm &= lm - 1u;
+            k = nd->child[c];
+            kend = k + nd->count[c];
+            if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)(kend - k);
+        }
+        const int w0 = win, k0 = kind;
+        tri_test<COUNT, false>(kp, k, o, d, best, kind, win, win_orig);
+        hit = hit || win != w0 || kind != k0;
+        ++k;
+    }
+    if (next >= 0) {
+        node = next;
+        return true;
+    }
+    if (sp == 0) return false;
+    --sp;
+    node = stk[sp * 256];
+    return true;
+}
+
+template <bool COUNT, bool SKY>
+__device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, uint32_t pixel, int s0, int s1,
+                                             uint32_t* rng, double* acc, Cnt& cnt)
+{
+    constexpr int QW = 256;                      // < 64 entries + 3 pushes x 64 lanes
+    __shared__ unsigned lifo_lds[4][QW];
+    volatile unsigned* q = lifo_lds[threadIdx.x >> 6];
+    unsigned short* stk = bvh_stack();
+    const int lane = threadIdx.x & 63;
+    LanePath<COUNT, SKY> L;
+    L.init(s0, s1);
+    while (L.state != SM_DONE) {
+        if (L.state == SM_RESOLVE) L.resolve(kp, acc, cnt);
+        if (L.state == SM_CAM) L.start(kp, x, g, pixel, s1, rng, acc, cnt);
+        if (L.state == SM_CAST) {
+            L.cast(kp, cnt);
+            L.trav(kp, stk, 1, cnt);             // the root node; SM_TRAV: parked
+        }
+        const unsigned long long parked = __ballot(L.state == SM_TRAV);
+        const unsigned long long movable = __ballot(L.state == SM_RESOLVE || L.state == SM_CAM);
+        if (parked == 0ull || (__popcll(parked) < RT_BVH_COOP && movable != 0ull)) continue;
+
+        // ---- cooperative phase (wave-uniform) ----
+        int qn = 0;
+        {
+            unsigned it[4];
+            int n = 0;
+            if (L.state == SM_TRAV) {            // next node + the root's pushes (sp <= 3)
+                it[0] = (unsigned)lane | ((unsigned)L.node << 6);
+                for (int j = 0; j < L.sp; ++j) it[1 + j] = (unsigned)lane | ((unsigned)stk[j * 256] << 6);
+                n = 1 + L.sp;
+            }
+            lifo_push(q, qn, n, it);
+        }
+        bool has = false;
+        int tr = 0, tnode = 0, tsp = 0;
+        V3 to = v3(0, 0, 0), td = to, tinv = to;
+        for (;;) {
+            const unsigned long long idle = __ballot(!has);
+            const int take = min(__popcll(idle), qn);
+            bool fresh = false;
+            if (!has) {
+                const int rank = __popcll(idle & lanes_below());
+                if (rank < take) {
+                    const unsigned item = q[qn - 1 - rank];
+                    tr = (int)(item & 63u);
+                    tnode = (int)(item >> 6);
+                    tsp = 0;
+                    has = true;
+                    fresh = true;
+                }
+            }
+            qn -= take;
+            __builtin_amdgcn_wave_barrier();
+            if (__ballot(has) == 0ull) break;
+            // the owner's ray for new tasks, its current record for every task
+            // (all live lanes run the permutes; owners are live)
+            if (__ballot(fresh) != 0ull) {
+                const V3 ro = v3(shfl_d(L.o.x, tr), shfl_d(L.o.y, tr), shfl_d(L.o.z, tr));
+                const V3 rd = v3(shfl_d(L.cd.x, tr), shfl_d(L.cd.y, tr), shfl_d(L.cd.z, tr));
+                if (fresh) {
+                    to = ro;
+                    td = rd;
+                    tinv = bvh_inv(rd);
+                }
+            }
+            double best = shfl_d(L.best, tr);
+            int kind = __shfl(L.kind, tr, 64), win = __shfl(L.win, tr, 64), win_orig = __shfl(L.win_orig, tr, 64);
+            bool hit = false;
+            unsigned push[3];
+            int npush = 0;
+            const bool to_lifo = qn < 64;
+            if (has) {
+                if (!coop_step<COUNT>(kp, to, td, tinv, stk, tnode, tsp, best, kind, win, win_orig, hit, to_lifo,
+                                      push, npush, cnt))
+                    has = false;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) push[j] = (unsigned)tr | (push[j] << 6);
+            }
+            lifo_push(q, qn, npush, push);
+            // merge the lanes' better triangles into their owners' records
+            unsigned long long m = __ballot(hit);
+            while (m != 0ull) {
+                const int l = __ffsll(m) - 1;
+                m &= m - 1ull;
+                const int r = __builtin_amdgcn_readlane(tr, l);
+                const double db = rl_d(best, l);
+                const int dw = __builtin_amdgcn_readlane(win, l), dorig = __builtin_amdgcn_readlane(win_orig, l);
+                if (lane == r && (db < L.best || (db == L.best && L.kind == HIT_TRI && dorig < L.win_orig))) {
+                    L.best = db;
+                    L.kind = HIT_TRI;
+                    L.win = dw;
+                    L.win_orig = dorig;
+                }
+            }
+        }
+        if (L.state == SM_TRAV) L.state = SM_RESOLVE;
+    }
+}
+#endif
+
 // Body of render_kernel (main.c semantics) and render_kernel_cuda
 // (main_cuda.cu's): one thread = (pixel, chunk of its samples).
 template <bool COUNT, bool BVH, bool SKY, bool CU>
@@ -1307,7 +1549,11 @@ __device__ __forceinline__ void render_body(const KParams& kp)
         const bool carry = !COUNT && kp.sums && kp.chunks == 1;
 #pragma unroll
         for (int j = 0; j < 9; ++j) acc[j * 256] = carry ? kp.sums[li * 9 + j] : 0.0;
-#if RT_BVH_SM > 0
+#if RT_BVH_COOP > 0
+        if constexpr (BVH && !CU) {
+            samples_coop<COUNT, SKY>(kp, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc, cnt);
+        } else
+#elif RT_BVH_SM > 0
         if constexpr (BVH && !CU) {
             samples_sm<COUNT, SKY>(kp, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc, cnt);
         } else

@@ -1,6 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/c4prof
+OUT=${OUT:-gpurun_out/c4prof}
 mkdir -p $OUT
 B="python3 tools/bench_configs.py --only C4 --spp-scale 0.5"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- $B > $OUT/kt.log 2>&1 &&
