@@ -265,6 +265,59 @@ def test_bvh_tie_break_on_duplicate_triangles():
     check_parity(bundle, helpers.params(24, 18, 2, 6, accel=1))
 
 
+def grazing_grid_scene(n=40, seed=11):
+    """A fine n x n quad grid (2 n^2 triangles) just above the README box's
+    floor, with a small random height on every vertex, seen from a low
+    camera: grazing rays cross many boxes, so the cooperative traversal's
+    per-wave LIFO and the lanes' own stacks both fill (rt_kernels.hip
+    samples_coop)."""
+    from tipe_rt.types import Triangle, Material, Vec3, UV
+    rng = np.random.default_rng(seed)
+    xs = np.linspace(-1.0, 1.0, n + 1)
+    zs = np.linspace(-3.5, -0.8, n + 1)
+    hgt = -0.95 + rng.uniform(0.0, 0.01, size=(n + 1, n + 1))
+    tris = (Triangle * (2 * n * n))()
+    qm = (C.c_int * (2 * n * n))()
+    t = 0
+    for i in range(n):
+        for j in range(n):
+            p00 = (xs[i], hgt[i, j], zs[j])
+            p10 = (xs[i + 1], hgt[i + 1, j], zs[j])
+            p01 = (xs[i], hgt[i, j + 1], zs[j + 1])
+            p11 = (xs[i + 1], hgt[i + 1, j + 1], zs[j + 1])
+            # counter-clockwise seen from above: N = AB x AC points up
+            for (a, b, c) in ((p00, p01, p10), (p10, p01, p11)):
+                tris[t].A, tris[t].B, tris[t].C = Vec3(*a), Vec3(*b), Vec3(*c)
+                tris[t].uvA = tris[t].uvB = tris[t].uvC = UV(0.5, 0.5)
+                qm[t] = (i + j) % 2
+                t += 1
+    mats = (Material * 2)()
+    # near-mirrors: reflected grazing rays stay grazing
+    mats[0] = tipe_rt.scenes.material((0.8, 0.8, 0.7), (0, 0, 0), 0.0, 0.97)
+    mats[1] = tipe_rt.scenes.material((0.2, 0.4, 0.8), (0, 0, 0), 0.0, 0.9)
+    return helpers.SceneBundle(tipe_rt.scenes.cornell_spheres(), (tris, qm, mats, 1, 1, 2))
+
+
+def test_bvh_grazing_grid_deep_traversal():
+    bundle = grazing_grid_scene()
+    cam = tipe_rt.init_camera((0.0, -0.9, -0.6), (0.0, -0.935, -3.0), (0, 1, 0), 40.0, 4.0 / 3.0)
+    check_parity(bundle, helpers.params(32, 24, 4, 6, cam=cam))
+    check_parity(bundle, helpers.params(24, 18, 2, 5, cam=cam, use_ao=True, ao=2.0))
+    import torch
+    p = helpers.params(32, 24, 4, 6, cam=cam)
+    ds = tipe_rt.DeviceScene(bundle.scene, 0)
+    d_cnt = torch.zeros(tipe_rt.RT_NCOUNTERS, dtype=torch.int64, device="cuda:0")
+    tipe_rt.count_async(ds, p, tipe_rt.band_tiling(0, 23), d_cnt.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ds.close()
+    c = d_cnt.cpu().numpy()
+    T = tipe_rt.types
+    print("grazing grid: node visits / cast", c[T.RT_CNT_BVH_NODES] / c[T.RT_CNT_CASTS],
+          "triangle tests / cast", c[T.RT_CNT_BVH_TRI_TESTS] / c[T.RT_CNT_CASTS])
+    # 2.4 node visits per cast of any kind here (sphere-only casts included)
+    assert c[T.RT_CNT_BVH_NODES] > 2 * c[T.RT_CNT_CASTS]
+
+
 def adversarial_sphere_scene():
     """Sphere pairs the candidate pass cannot separate (spheres_closest):
     an exact duplicate (equal t: the reference keeps the first), a sphere
