@@ -245,6 +245,17 @@ int rt_accumulate_async(const rt_device_scene* scene, const rt_params* params, l
 int rt_resolve_async(const double* d_sums, const rt_params* params, int total_spp, const rt_tiling* tiling,
                      const rt_frame* frame, void* hip_stream);
 
+/* ---- zero-throughput exit ------------------------------------------------ */
+/* tracer (main.c:118-242) keeps bouncing after rayColor has become (0, 0, 0)
+ * (a black-diffuse light, a green wall then a red one, an AO miss); those
+ * bounces add exactly 0.  Render launches end such paths early when that is
+ * provably exact for the scene and parameters (bounded materials, and with
+ * AO 0 < AO_intensity <= 1000 and coordinates within 2^20), so frames are
+ * bit-identical either way; only the work done, and so rt_count_async's
+ * cast/shade/draw counts, differ.  Process-wide, default on; 0 reproduces
+ * the reference's counts (tests).  Returns the previous setting. */
+int rt_set_zero_throughput_exit(int enable);
+
 /* ---- denoiser hook (denoiser.h:31-91, called at main.c:455) -------------- */
 /* denoiser()'s signature.  main.c runs it once on the finished frame when
  * useDenoiser is set; the OIDN library itself is not part of this one. */

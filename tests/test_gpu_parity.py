@@ -175,6 +175,46 @@ def test_spp_chunks_row_bands(monkeypatch):
     check_parity(helpers.cornell(), helpers.params(37, 53, 8, 5, chunks=4))
 
 
+@pytest.mark.parametrize("case", ["cornell", "cornell_ao", "pyramid", "sky", "bands", "one_sample_chunks"])
+def test_task_queue_kernel_bitexact(case, monkeypatch):
+    """spp_chunks > 1 without a BVH runs render_kernel_q: persistent lanes
+    take (chunk, pixel) tasks from a counter in whatever order the waves get
+    to them; the chunk partials, summed in chunk order, equal the oracle's."""
+    bundle, p = {
+        "cornell": lambda: (helpers.cornell(), helpers.params(96, 72, 24, 6, chunks=8)),
+        "cornell_ao": lambda: (helpers.cornell(), helpers.params(64, 48, 12, 6, use_ao=True, ao=2.5, compat=0,
+                                                                chunks=4)),
+        "pyramid": lambda: (helpers.pyramid_scene(), helpers.params(64, 48, 12, 6, chunks=6)),
+        "sky": lambda: (helpers.sky_scene(), helpers.params(48, 36, 9, 5, sky_mode=1, chunks=3)),
+        "bands": lambda: (helpers.cornell(), helpers.params(37, 53, 8, 5, chunks=4)),
+        "one_sample_chunks": lambda: (helpers.cornell(), helpers.params(33, 25, 5, 6, chunks=5)),
+    }[case]()
+    if case == "bands":
+        monkeypatch.setenv("RT_PARTIAL_BUDGET", str(16 * 37 * 4 * 72))
+    check_parity(bundle, p)
+
+
+def test_task_queue_kernel_cyclic_tiles():
+    """The queue kernel on a rank's cyclic row tiles (multi-GPU layout)."""
+    import torch
+    bundle = helpers.cornell()
+    W, H, k, world = 40, 30, 2, 3
+    p = helpers.params(W, H, 8, 5, chunks=4)
+    ref = helpers.oracle_render(bundle, p)
+    ds = tipe_rt.DeviceScene(bundle.scene, 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    per_rank = tipe_rt.cyclic_tiling(H, k, 0, world).n_tiles
+    gathered = torch.zeros((world, per_rank * k, W, 3), dtype=torch.float64, device="cuda:0")
+    for r in range(world):
+        t = tipe_rt.cyclic_tiling(H, k, r, world)
+        tipe_rt.render_async(ds, p, t, gathered[r].data_ptr(), stream=stream)
+    full = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda:0")
+    tipe_rt.assemble_async(gathered.data_ptr(), world, k, per_rank * k, W, H, full.data_ptr(), stream)
+    torch.cuda.synchronize()
+    ds.close()
+    assert (full.cpu().numpy() == ref["canva"]).all()
+
+
 def test_spp_chunks_only_move_the_last_bits():
     bundle = helpers.cornell()
     a = helpers.oracle_render(bundle, helpers.params(24, 18, 16, 6))
@@ -425,14 +465,69 @@ def test_counters_match_oracle():
     ref = helpers.oracle_render(bundle, p, counters=True)["counters"]
     ds = tipe_rt.DeviceScene(bundle.scene, 0)
     d_cnt = torch.zeros(tipe_rt.RT_NCOUNTERS, dtype=torch.int64, device="cuda:0")
-    tipe_rt.count_async(ds, p, tipe_rt.band_tiling(0, 23), d_cnt.data_ptr(),
-                        torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
+    with tipe_rt.reference_counts():
+        tipe_rt.count_async(ds, p, tipe_rt.band_tiling(0, 23), d_cnt.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
     got = d_cnt.cpu().numpy().astype(np.uint64)
     ds.close()
     k = tipe_rt.types.RT_CNT_EXACT_RESCANS           # GPU-only diagnostic
     assert list(got[:k]) == list(ref[:k]), dict(zip(tipe_rt.COUNTER_NAMES, zip(got, ref)))
     assert got[k] <= got[tipe_rt.types.RT_CNT_CASTS] // 1000   # candidate pass almost never ambiguous
+
+
+def _counts(bundle, p, rows):
+    import torch
+    ds = tipe_rt.DeviceScene(bundle.scene, 0)
+    d_cnt = torch.zeros(tipe_rt.RT_NCOUNTERS, dtype=torch.int64, device="cuda:0")
+    tipe_rt.count_async(ds, p, tipe_rt.band_tiling(0, rows - 1), d_cnt.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ds.close()
+    return d_cnt.cpu().numpy()
+
+
+@pytest.mark.parametrize("scene,ao", [("cornell", False), ("cornell", True), ("pyramid", True), ("tree", True)])
+def test_zero_throughput_exit(scene, ao):
+    """Paths end once rayColor == 0 (rt_set_zero_throughput_exit): frames are
+    bit-identical with the exit on and off and to the oracle (which never
+    exits), and the exit only removes casts."""
+    bundle = {"cornell": helpers.cornell, "pyramid": helpers.pyramid_scene, "tree": helpers.tree_scene}[scene]()
+    p = helpers.params(32, 24, 8, 6, use_ao=ao, ao=2.5, compat=0)
+    check_parity(bundle, p)
+    on = gpu_render(bundle, p)
+    with tipe_rt.reference_counts():
+        off = gpu_render(bundle, p)
+        ref_cnt = _counts(bundle, p, 24)
+    for a, b in zip(on, off):
+        assert_same(a, b, "exit on vs off")
+    cnt = _counts(bundle, p, 24)
+    T = tipe_rt.types
+    assert cnt[T.RT_CNT_SAMPLES] == ref_cnt[T.RT_CNT_SAMPLES]
+    assert cnt[T.RT_CNT_CASTS] < ref_cnt[T.RT_CNT_CASTS]
+    print(scene, "ao" if ao else "", "casts per sample", ref_cnt[T.RT_CNT_CASTS] / ref_cnt[0], "->",
+          cnt[T.RT_CNT_CASTS] / cnt[0])
+
+
+def test_zero_throughput_exit_gated_off():
+    """A material beyond the exit's bound (emission strength 1e200 > 2^100:
+    the host cannot rule out em overflowing to inf, and inf * 0 is NaN) or
+    AO_intensity outside (0, 1000] turns the exit off: the counts are then
+    the reference's."""
+    spheres = tipe_rt.scenes.cornell_spheres()
+    spheres[3].mat.emissionStrength = 1e200
+    bundle = helpers.SceneBundle(spheres)
+    p = helpers.params(16, 12, 4, 6)
+    check_parity(bundle, p)
+    ref = helpers.oracle_render(bundle, p, counters=True)["counters"]
+    cnt = _counts(bundle, p, 12)
+    assert cnt[tipe_rt.types.RT_CNT_CASTS] == ref[tipe_rt.types.RT_CNT_CASTS]
+    bundle = helpers.cornell()
+    p = helpers.params(16, 12, 4, 6, use_ao=True, ao=2000.0, compat=0)
+    check_parity(bundle, p)
+    ref = helpers.oracle_render(bundle, p, counters=True)["counters"]
+    cnt = _counts(bundle, p, 12)
+    assert cnt[tipe_rt.types.RT_CNT_CASTS] == ref[tipe_rt.types.RT_CNT_CASTS]
 
 
 # ---- boundary behaviour --------------------------------------------------------

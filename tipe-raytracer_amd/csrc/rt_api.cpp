@@ -143,9 +143,22 @@ struct rt_device_scene {
     int* tri_orig = nullptr;         // leaf order -> caller's triangle index
     int bvh_nodes = 0, bvh_depth = 0;
     double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0;
+    bool mats_bounded = false;       // every diffuse/emission/strength finite, |x| <= 2^100
+    double coord_max = HUGE_VAL;     // max |coordinate| of the spheres (|C_a| + R) and triangle vertices
 };
 
 namespace {
+
+std::atomic<int> g_zero_exit{1};
+
+// The shading fields a zero rayColor multiplies (LanePath::zero_rc).
+bool shading_bounded(const DevMat& m)
+{
+    const double v[7] = {m.dr, m.dg, m.db, m.er, m.eg, m.eb, m.es};
+    for (double x : v)
+        if (!(std::fabs(x) <= 0x1p100)) return false;
+    return true;
+}
 
 DevMat to_dev(const rt_material& m)
 {
@@ -257,6 +270,10 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     double cam = 0.0;
     for (int i = 0; i < 3; ++i) cam = std::max(cam, std::fabs(p->cam.origin.e[i]));
     cam += 0.5 * (std::fabs(ox) + std::fabs(oy));
+    // Zero-throughput exit (rt_kernels.hip LanePath::zero_rc): exact when the
+    // shading values are bounded and, with AO, the AO factor stays finite.
+    kp.zero_exit = g_zero_exit.load() && p->semantics != RT_SEM_CUDA && sc->mats_bounded &&
+                   (!kp.useAO || (AO > 0.0 && AO <= 1000.0 && std::fmax(sc->coord_max, cam) <= 0x1p20));
     if (sc->bvh && p->accel == RT_ACCEL_AUTO && cam <= sc->r_scene) {
         kp.bvh = sc->bvh;
         kp.bvh_srel = sc->s_rel;
@@ -293,7 +310,8 @@ int launch_on_stream(KParams& kp, const double* uni, hipStream_t st, bool count)
     }
     double* d_uni = nullptr;
     double* d_part = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&d_uni, U_COUNT * sizeof(double), st));
+    // uniform block + render_kernel_q's task counter (on its own 64-byte line)
+    HIP_TRY(hipMallocAsync((void**)&d_uni, (U_COUNT + 16) * sizeof(double), st));
     UniBlock ub;
     for (int i = 0; i < U_COUNT; ++i) ub.v[i] = uni[i];
     hipError_t e = (hipError_t)launch_set_uniforms(ub, d_uni, st);
@@ -310,6 +328,10 @@ int launch_on_stream(KParams& kp, const double* uni, hipStream_t st, bool count)
     }
     kp.uni = d_uni;
     kp.partial = d_part;
+    // the queue kernel numbers tasks (chunk, pixel of the band) in 32 bits
+    // the queue kernel numbers tasks (chunk, pixel of the band) in 32 bits
+    kp.task_ctr = (d_part && (unsigned long long)band * kp.W * kp.chunks < (1ull << 31))
+                      ? (unsigned*)(d_uni + ((U_COUNT + 7) / 8 + 1) * 8) : nullptr;
     for (int y0 = 0; e == hipSuccess && y0 < kp.local_rows; y0 += band) {
         kp.band_y0 = y0;
         kp.band_rows = band;
@@ -497,8 +519,26 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         for (long long i = 0; i < n_texels; ++i) texels[(size_t)i] = to_dev(scene->mat_list[i]);
     }
 
+    bool mats_bounded = true;
+    double coord_max = 0.0;
+    for (const DevMat& m : sph_mat) mats_bounded = mats_bounded && shading_bounded(m);
+    for (const DevMat& m : texels) mats_bounded = mats_bounded && shading_bounded(m);
+    for (const DevMat& m : sky) mats_bounded = mats_bounded && shading_bounded(m);
+    for (int i = 0; i < scene->nbSpheres; ++i) {
+        const rt_sphere& q = scene->sphere_list[i];
+        for (int a = 0; a < 3; ++a) coord_max = std::fmax(coord_max, std::fabs(q.center.e[a]) + std::fabs(q.radius));
+        if (!std::isfinite(q.radius)) coord_max = HUGE_VAL;
+    }
+    for (int i = 0; i < scene->nbTriangles; ++i) {
+        const rt_triangle& t = scene->triangle_list[i];
+        for (int a = 0; a < 3; ++a)
+            coord_max = std::fmax(coord_max, std::fmax(std::fabs(t.A.e[a]), std::fmax(std::fabs(t.B.e[a]), std::fabs(t.C.e[a]))));
+    }
+
     rt_device_scene* ds = new rt_device_scene();
     ds->device = device;
+    ds->mats_bounded = mats_bounded;
+    ds->coord_max = coord_max;
     ds->ns = scene->nbSpheres;
     ds->ns_pad = ns_pad;
     ds->cand_lmax = cand_lmax;
@@ -737,6 +777,7 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, i
 }
 
 void rt_set_denoise_hook(rt_denoise_fn fn) { g_denoise.store(fn); }
+int rt_set_zero_throughput_exit(int enable) { return g_zero_exit.exchange(enable ? 1 : 0); }
 rt_denoise_fn rt_get_denoise_hook(void) { return g_denoise.load(); }
 
 int rt_denoise_pack(int W, int H, const rt_color* canva, const rt_color* albedo, const rt_color* normal,

@@ -87,6 +87,7 @@ struct KParams {
     // image / integrator
     int W, H, S, B;
     int useAO;
+    int zero_exit;           // paths end once rayColor == 0 (host: only where exact, LanePath::zero_rc)
     uint32_t key0, key1;
     int chunks;              // samples of a pixel split into this many chunks
     // tiling
@@ -101,6 +102,8 @@ struct KParams {
     double* partial;         // chunks > 1: [chunks][band_rows*W][9]
     double* sums;            // accumulate mode (rt_accumulate_async): [local_rows*W][9] running sums, or null
     long long s_base;        // global index of this launch's first sample (Philox counter word 3)
+    unsigned* task_ctr;      // render_kernel_q's task counter (zeroed per band launch), or null
+    unsigned long long* trace;   // render_kernel_q diagnostics (RT_QUEUE_TRACE), normally null
     unsigned long long* counters;
 };
 

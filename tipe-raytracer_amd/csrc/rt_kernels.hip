@@ -40,6 +40,9 @@
 //    grouping that the oracle reproduces).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
 
 #include "rt/rt.h"
 #include "rt_internal.h"
@@ -68,6 +71,15 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #endif
 #ifndef RT_BVH_COOP                 // BVH kernel: wave-cooperative deep traversal once this many
 #define RT_BVH_COOP 1               // lanes wait for it (0: off, samples_sm)
+#endif
+#ifndef RT_FLAT                     // sphere kernel: sample loop as LanePath rounds (0: nested trace())
+#define RT_FLAT 1
+#endif
+#ifndef RT_FLAT_FILL                // ... camera rays start once this many eighths of the live lanes wait
+#define RT_FLAT_FILL 2
+#endif
+#ifndef RT_QUEUE                    // sphere kernel, spp_chunks > 1: persistent lanes + (chunk, pixel) task queue
+#define RT_QUEUE 64                 // (tasks per atomic grab of a wave; 0: off)
 #endif
 #ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
 #define RT_WAVES_PER_SIMD_BVH 3
@@ -1058,6 +1070,22 @@ struct LanePath {
     int i, kind, win, win_orig, node, sp, s, state;
     bool chain, ao_cast;
 
+    // Zero-throughput exit (kp.zero_exit, set by the host only when it is
+    // exact): once rayColor is (0, 0, 0) every later bounce adds em * 0 = +-0
+    // to incomingLight (x + +-0 == x: incomingLight starts at +0 and is never
+    // -0), multiplies rayColor by a finite diffuse colour or AO factor (still
+    // 0), and chain (albedo/normal) is already off, since rayColor only
+    // changes after it is cleared.  Draws are counter-based per sample, so
+    // skipping the rest of the path changes no other sample.  The host
+    // requires every emission, strength and diffuse value finite with
+    // |x| <= 2^100 (no em overflow), and with AO 0 < AO_intensity <= 1000
+    // and every coordinate within 2^20 (the AO factor pow(distance/dst, AO)/AO
+    // then stays finite: distance/dst <= 1.02).
+    __device__ __forceinline__ bool zero_rc(const KParams& kp) const
+    {
+        return kp.zero_exit && rc.x == 0.0 && rc.y == 0.0 && rc.z == 0.0;
+    }
+
     __device__ __forceinline__ void init(int s0, int s1)
     {
         o = d = cd = inc = rc = inv = v3(0, 0, 0);
@@ -1094,6 +1122,7 @@ struct LanePath {
             occ = (occ / 1.0) / AO;
             rc = mulv(rc, v3(occ, occ, occ));
             ao_cast = false;
+            if (zero_rc(kp)) more = false;   // an AO miss zeroes rayColor: nothing more to add
         } else if (kind == HIT_NONE) {       // miss: the path ends, main.c:236-238
             if (chain) {
                 acc_add(acc, ACC_ALB, v3(0, 0, 0));
@@ -1183,6 +1212,10 @@ struct LanePath {
                         if (r.x > 0.5 || r.y > 0.5 || r.z > 0.5) r = mulv(mat.diff, muls(r, 1.3));
                         rc = mulv(mat.diff, r);
                     }
+                    if (zero_rc(kp)) {           // black diffuse (a light, a green-then-red wall)
+                        ao_cast = false;         // the AO cast could only scale 0
+                        more = false;
+                    }
                 }
             }
         }
@@ -1239,6 +1272,13 @@ struct LanePath {
         }
     }
 
+    // the whole cast without a BVH (spheres + brute-force triangles)
+    __device__ __forceinline__ void cast_flat(const KParams& kp, Cnt& cnt)
+    {
+        kind = closest_hit<COUNT, false>(kp, o, cd, best, win, cnt);
+        state = SM_RESOLVE;
+    }
+
     // closest_hit's sphere half and the traversal set-up
     __device__ __forceinline__ void cast(const KParams& kp, Cnt& cnt)
     {
@@ -1285,6 +1325,33 @@ __device__ __forceinline__ void samples_sm(const KParams& kp, int x, int g, uint
 }
 #endif
 
+
+#if RT_FLAT > 0
+// The sphere kernel's sample loop as LanePath rounds (RT_FLAT > 0): each
+// round every lane with a path casts and shades one bounce; a lane whose path
+// ended (a miss, a light seen directly, the bounce budget, or zero
+// throughput) waits for its next sample's camera ray, which starts once
+// RT_FLAT_FILL eighths of the wave's live lanes wait (the camera ray then
+// costs the wave one pass for many lanes).  Same casts, draws and sums per
+// sample as trace(), so bit-identical; it lets the zero-throughput exit
+// save the cast instead of idling the lane until the wave's longest path.
+template <bool COUNT, bool SKY>
+__device__ __forceinline__ void samples_flat(const KParams& kp, int x, int g, uint32_t pixel, int s0, int s1,
+                                             uint32_t* rng, double* acc, Cnt& cnt)
+{
+    LanePath<COUNT, SKY> L;
+    L.init(s0, s1);
+    while (L.state != SM_DONE) {
+        const unsigned long long live = __ballot(1), wait = __ballot(L.state == SM_CAM);
+        const bool go = wait == live || __popcll(wait) * 8 >= __popcll(live) * RT_FLAT_FILL;
+        if (go && L.state == SM_CAM) L.start(kp, x, g, pixel, s1, rng, acc, cnt);
+        if (L.state == SM_CAST) {
+            L.cast_flat(kp, cnt);
+            L.resolve(kp, acc, cnt);
+        }
+    }
+}
+#endif
 
 #if RT_BVH_COOP > 0
 // Wave-cooperative traversal of the deep casts (RT_BVH_COOP > 0).  About 5 %
@@ -1558,6 +1625,11 @@ __device__ __forceinline__ void render_body(const KParams& kp)
             samples_sm<COUNT, SKY>(kp, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc, cnt);
         } else
 #endif
+#if RT_FLAT > 0
+        if constexpr (!BVH && !CU) {
+            samples_flat<COUNT, SKY>(kp, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc, cnt);
+        } else
+#endif
         for (int s = s0; s < s1; ++s) {
             Stream st;
             st.start(pixel, (uint32_t)(kp.s_base + s), kp.key0, kp.key1, rng_lds + threadIdx.x);
@@ -1611,6 +1683,111 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
 {
     render_body<COUNT, BVH, false, true>(kp);
 }
+
+#if RT_QUEUE > 0
+// Persistent sphere kernel over (chunk, pixel) tasks (RT_QUEUE > 0;
+// spp_chunks > 1, no BVH, main.c semantics).  A task is one pixel's samples
+// [c*S/P, (c+1)*S/P) in order, summed in the lane's LDS column and written to
+// the chunk partials, which combine_kernel sums in chunk order: the result is
+// the fixed-grid kernel's bit for bit whichever lane runs the task.  Paths
+// run as LanePath rounds (samples_flat); a lane whose task is done starts its
+// next one, so lanes with short paths (misses, lights, zero throughput) do
+// not idle until the wave's longest slice ends.
+// Tasks come from a per-launch counter, RT_QUEUE tasks per atomic: a wave
+// takes a batch and hands its tasks to its lanes as they need them.  Static
+// task lists were 1.3x slower: the dispatcher places waves unevenly over the
+// SIMDs (per-lane clocks: waves with the same work ended between 21 and
+// 45 ms), so only a dynamic queue keeps every SIMD busy to the end; one
+// atomic per lane grab was 1.8x slower (same-address atomics).  The grid is
+// the resident capacity; every lane leaves once the counter passes the
+// task count.
+template <bool SKY>
+__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel_q(const KParams kp)
+{
+    __shared__ double acc_lds[ACC_INC * 256];
+    __shared__ uint32_t rng_lds[4 * 256];
+    double* acc = acc_lds + threadIdx.x;
+    uint32_t* rng = rng_lds + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    Cnt cnt;
+    const unsigned npx = (unsigned)kp.band_rows * (unsigned)kp.W;
+    const unsigned ntask = npx * (unsigned)kp.chunks;
+    unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
+    LanePath<false, SKY> L;
+    L.init(0, 1);                    // SM_CAM with s = 0 >= s1 = 0: takes a task first
+    int x = 0, g = 0, s1 = 0;
+    unsigned chunk = 0, p = 0, pixel = 0;
+    bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
+    const long long t_start = kp.trace ? wall_clock64() : 0;
+    unsigned rounds = 0, ntasks = 0;
+    while (L.state != SM_DONE) {
+        ++rounds;
+        const unsigned long long live = __ballot(1), wait = __ballot(L.state == SM_CAM);
+        const bool go = wait == live || __popcll(wait) * 8 >= __popcll(live) * RT_FLAT_FILL;
+        const bool need = go && L.state == SM_CAM && L.s >= s1;
+        const unsigned long long nm = __ballot(need);
+        unsigned t = 0;
+        if (nm) {                    // wave-uniform: tasks for the lanes that need one
+            const unsigned n = (unsigned)__popcll(nm), avail = qe - qb;
+            const unsigned rank = (unsigned)__popcll(nm & ((1ull << lane) - 1ull));
+            if (avail < n) {         // a new batch (n <= 64 <= RT_QUEUE): old tasks first
+                unsigned nb = 0;
+                if (lane == __ffsll((long long)nm) - 1) nb = atomicAdd(kp.task_ctr, (unsigned)RT_QUEUE);
+                nb = __shfl(nb, __ffsll((long long)nm) - 1, 64);
+                t = rank < avail ? qb + rank : nb + (rank - avail);
+                qb = nb + (n - avail);
+                qe = nb + RT_QUEUE;
+            } else {
+                t = qb + rank;
+                qb += n;
+            }
+        }
+        if (need) {
+            ++ntasks;
+            if (owns) {              // task done: its sums to the chunk partials
+                double* q = kp.partial + ((size_t)chunk * npx + p) * 9;
+#pragma unroll
+                for (int j = 0; j < 9; ++j) q[j] = acc[j * 256];
+                owns = false;
+            }
+            if (t >= ntask) {
+                L.state = SM_DONE;
+            } else {
+                chunk = t / npx;
+                p = t - chunk * npx;
+                const int ly = kp.band_y0 + (int)(p / (unsigned)kp.W);
+                x = (int)(p % (unsigned)kp.W);
+                bool valid = ly < kp.local_rows;
+                if (valid) {
+                    const int lt = ly / kp.tile_rows, yy = ly - lt * kp.tile_rows;
+                    g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + yy;
+                    valid = g < kp.row_end;
+                }
+                if (valid) {         // otherwise the lane takes its next task next time
+                    pixel = (uint32_t)g * (uint32_t)kp.W + (uint32_t)x;
+                    L.s = (int)(((long long)chunk * kp.S) / kp.chunks);
+                    s1 = (int)(((long long)(chunk + 1) * kp.S) / kp.chunks);
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
+                    owns = true;
+                }
+            }
+        }
+        if (go && L.state == SM_CAM && L.s < s1) L.start(kp, x, g, pixel, s1, rng, acc, cnt);
+        if (L.state == SM_CAST) {
+            L.cast_flat(kp, cnt);
+            L.resolve(kp, acc, cnt);
+        }
+    }
+    if (kp.trace) {                  // diagnostics (RT_QUEUE_TRACE): per lane start, end, rounds, tasks
+        unsigned long long* q = kp.trace + ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+        q[0] = (unsigned long long)t_start;
+        q[1] = (unsigned long long)wall_clock64();
+        q[2] = rounds;
+        q[3] = ntasks;
+    }
+}
+#endif
 
 // Sum the chunk partials of each pixel in chunk order, then resolve.
 __global__ __launch_bounds__(256) void combine_kernel(const KParams kp)
@@ -1799,8 +1976,54 @@ static void launch_variant(const KParams& kp, void* stream)
     else hipLaunchKernelGGL((render_kernel<COUNT, false, false>), g, dim3(256), 0, st, kp);
 }
 
+#if RT_QUEUE > 0
+// Resident blocks of the queue kernel on this device (grid of render_kernel_q).
+static unsigned queue_grid(bool sky)
+{
+    static int cached[2][64];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    int& c = cached[sky ? 1 : 0][dev & 63];
+    if (c <= 0) {
+        int nb = 0, ncu = 0;
+        if (sky) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<true>, 256, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<false>, 256, 0);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        c = std::max(1, nb) * std::max(1, ncu);
+        if (const char* e = std::getenv("RT_QUEUE_BLOCKS")) c = std::max(1, std::atoi(e));   // experiments
+        if (std::getenv("RT_QUEUE_VERBOSE")) std::fprintf(stderr, "render_kernel_q: %d blocks/CU x %d CUs -> %d\n", nb, ncu, c);
+    }
+    return (unsigned)c;
+}
+#endif
+
 int launch_render(const KParams& kp, void* stream)
 {
+#if RT_QUEUE > 0
+    if (kp.task_ctr && kp.chunks > 1 && !kp.bvh && !kp.cuda && !kp.sums) {
+        const hipStream_t st = (hipStream_t)stream;
+        const bool sky = kp.sky != nullptr;
+        (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
+        const unsigned nb = queue_grid(sky);
+        unsigned long long* tr = nullptr;
+        const char* tf = std::getenv("RT_QUEUE_TRACE");
+        if (tf) (void)hipMalloc((void**)&tr, (size_t)nb * 256 * 4 * sizeof(unsigned long long));
+        KParams k2 = kp;
+        k2.trace = tr;
+        if (sky) hipLaunchKernelGGL(render_kernel_q<true>, dim3(nb), dim3(256), 0, st, k2);
+        else hipLaunchKernelGGL(render_kernel_q<false>, dim3(nb), dim3(256), 0, st, k2);
+        if (tr) {
+            std::vector<unsigned long long> h((size_t)nb * 256 * 4);
+            (void)hipStreamSynchronize(st);
+            (void)hipMemcpy(h.data(), tr, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+            (void)hipFree(tr);
+            if (FILE* f = std::fopen(tf, "ab")) {
+                std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+                std::fclose(f);
+            }
+        }
+    } else
+#endif
     launch_variant<false>(kp, stream);
     if (kp.chunks > 1) {
         const long long npx = (long long)kp.band_rows * kp.W;

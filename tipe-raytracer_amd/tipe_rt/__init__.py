@@ -64,6 +64,8 @@ def lib():
         L.rt_resolve_async.argtypes = [C.c_void_p, P(Params), C.c_int, P(Tiling), P(Frame), C.c_void_p]
         L.rt_set_denoise_hook.argtypes = [DENOISE_FN]
         L.rt_get_denoise_hook.restype = C.c_void_p
+        L.rt_set_zero_throughput_exit.argtypes = [C.c_int]
+        L.rt_set_zero_throughput_exit.restype = C.c_int
         L.rt_denoise_pack.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6
         L.rt_denoise_unpack.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.rt_denoise_pack_async.argtypes = [C.c_int, C.c_int, P(Frame)] + [C.c_void_p] * 4
@@ -76,11 +78,30 @@ EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error",
                     "rt_scene_release", "rt_render_async", "rt_assemble_async", "rt_count_async",
                     "rt_selftest_math", "rt_accumulate_async", "rt_resolve_async", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
                     "rt_denoise_unpack", "rt_denoise_pack_async", "rt_verify_sampler_phi",
-                    "rt_verify_sphere_pass"]
+                    "rt_verify_sphere_pass", "rt_set_zero_throughput_exit"]
 
 # rt_denoise_fn (rt.h): denoiser()'s signature, denoiser.h:31
 DENOISE_FN = C.CFUNCTYPE(None, C.c_int, C.c_int, C.c_void_p, Camera, C.c_void_p, C.c_void_p)
 _hook_ref = None
+
+
+def set_zero_throughput_exit(enable):
+    """rt_set_zero_throughput_exit (rt.h): end paths whose rayColor is exactly
+    0 where that is exact (default on; frames are identical either way, only
+    the counted work differs).  Returns the previous setting."""
+    return bool(lib().rt_set_zero_throughput_exit(1 if enable else 0))
+
+
+class reference_counts:
+    """Context manager: zero-throughput exit off, so rt_count_async counts
+    what the reference's tracer does (the oracle's counters)."""
+    def __enter__(self):
+        self.prev = set_zero_throughput_exit(False)
+        return self
+
+    def __exit__(self, *exc):
+        set_zero_throughput_exit(self.prev)
+        return False
 
 
 def set_denoise_hook(fn):
