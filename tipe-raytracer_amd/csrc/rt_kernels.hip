@@ -78,8 +78,14 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_FLAT_FILL                // ... camera rays start once this many eighths of the live lanes wait
 #define RT_FLAT_FILL 2
 #endif
+#ifndef RT_QUEUE_FILL               // queue kernel: camera rays once this many eighths of the lanes wait or lack one
+#define RT_QUEUE_FILL 4
+#endif
 #ifndef RT_QUEUE                    // sphere kernel, spp_chunks > 1: persistent lanes + (chunk, pixel) task queue
 #define RT_QUEUE 64                 // (tasks per atomic grab of a wave; 0: off)
+#endif
+#ifndef RT_PREFETCH                 // queue kernel: camera rays computed one path ahead (LDS)
+#define RT_PREFETCH 1
 #endif
 #ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
 #define RT_WAVES_PER_SIMD_BVH 3
@@ -1022,8 +1028,22 @@ __device__ __forceinline__ void write_pixel(const KParams& kp, long long li, V3 
 }
 
 // Primary ray of sample st (main.c:258-270; camera.h:42-55 get_ray).
-template <bool CU>
-__device__ __forceinline__ void camera_ray(const KParams& kp, int x, int g, Stream& st, V3& no, V3& rd)
+// The four camera draws of a sample (draws 0-3: word n of Philox block 0)
+// from registers, for a camera ray computed ahead of its path
+// (render_kernel_q): the lane's LDS block cache stays with the path in flight.
+struct CamDraws {
+    Philox b;
+    int n;
+    __device__ __forceinline__ uint32_t next31()
+    {
+        const uint32_t w = n == 0 ? b.w0 : n == 1 ? b.w1 : n == 2 ? b.w2 : b.w3;
+        ++n;
+        return w >> 1;
+    }
+};
+
+template <bool CU, class ST>
+__device__ __forceinline__ void camera_ray(const KParams& kp, int x, int g, ST& st, V3& no, V3& rd)
 {
     const double ju = -0.5 + 1.0 * unit31(st.next31());     // randomDouble(-0.5, 0.5)
     const double jv = -0.5 + 1.0 * unit31(st.next31());
@@ -1277,6 +1297,25 @@ struct LanePath {
     {
         kind = closest_hit<COUNT, false>(kp, o, cd, best, win, cnt);
         state = SM_RESOLVE;
+    }
+
+    // start() for a camera ray computed ahead (draws 0-3 of sample s used):
+    // the path's stream resumes at draw 4 (Philox block 1)
+    __device__ __forceinline__ void begin(const KParams& kp, uint32_t pixel, V3 no, V3 rd, uint32_t* rng, double* acc,
+                                          Cnt& cnt)
+    {
+        st.start(pixel, (uint32_t)(kp.s_base + s), kp.key0, kp.key1, rng);
+        st.n = 4;
+        o = no;
+        d = rd;
+        cd = rd;
+        inc = v3(0, 0, 0);
+        rc = v3(1, 1, 1);
+        top_n2 = 1.0;
+        i = 0;
+        chain = true;
+        ao_cast = false;
+        state = SM_CAST;                 // kp.B > 0 (the queue kernel's prefetch is off otherwise)
     }
 
     // closest_hit's sphere half and the traversal set-up
@@ -1705,13 +1744,17 @@ template <bool SKY>
 __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel_q(const KParams kp)
 {
     __shared__ double acc_lds[ACC_INC * 256];
+    __shared__ double pf_lds[(RT_PREFETCH ? 6 : 1) * 256];   // a camera ray computed ahead (o, d)
     __shared__ uint32_t rng_lds[4 * 256];
     double* acc = acc_lds + threadIdx.x;
     uint32_t* rng = rng_lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
     Cnt cnt;
-    const unsigned npx = (unsigned)kp.band_rows * (unsigned)kp.W;
-    const unsigned ntask = npx * (unsigned)kp.chunks;
+    const unsigned npx = (unsigned)kp.band_rows * (unsigned)kp.W;     // partials' chunk stride
+    // tasks cover the rows of this band that exist (the last band is shorter)
+    const int rows_here = min(kp.band_rows, kp.local_rows - kp.band_y0);
+    const unsigned npx_here = (unsigned)max(rows_here, 0) * (unsigned)kp.W;
+    const unsigned ntask = npx_here * (unsigned)kp.chunks;
     unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
     LanePath<false, SKY> L;
     L.init(0, 1);                    // SM_CAM with s = 0 >= s1 = 0: takes a task first
@@ -1720,10 +1763,18 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel_q(const 
     bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
     const long long t_start = kp.trace ? wall_clock64() : 0;
     unsigned rounds = 0, ntasks = 0;
+    int pf_s = -1;                   // sample whose camera ray waits in pf (this task), or -1
+    double* pf = pf_lds + threadIdx.x;
+    const bool prefetch = RT_PREFETCH && kp.B > 0;
     while (L.state != SM_DONE) {
         ++rounds;
+        if (L.state == SM_CAM && pf_s == L.s) {     // path done, next sample's ray is ready
+            L.begin(kp, pixel, lds_get(pf, 0), lds_get(pf, 3), rng, acc, cnt);
+            pf_s = -1;
+        }
         const unsigned long long live = __ballot(1), wait = __ballot(L.state == SM_CAM);
-        const bool go = wait == live || __popcll(wait) * 8 >= __popcll(live) * RT_FLAT_FILL;
+        const unsigned long long lack = __ballot(prefetch && L.state == SM_CAST && pf_s < 0 && L.s + 1 < s1);
+        const bool go = wait == live || (__popcll(wait) + __popcll(lack)) * 8 >= __popcll(live) * RT_QUEUE_FILL;
         const bool need = go && L.state == SM_CAM && L.s >= s1;
         const unsigned long long nm = __ballot(need);
         unsigned t = 0;
@@ -1753,8 +1804,8 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel_q(const 
             if (t >= ntask) {
                 L.state = SM_DONE;
             } else {
-                chunk = t / npx;
-                p = t - chunk * npx;
+                chunk = t / npx_here;
+                p = t - chunk * npx_here;
                 const int ly = kp.band_y0 + (int)(p / (unsigned)kp.W);
                 x = (int)(p % (unsigned)kp.W);
                 bool valid = ly < kp.local_rows;
@@ -1773,7 +1824,25 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel_q(const 
                 }
             }
         }
-        if (go && L.state == SM_CAM && L.s < s1) L.start(kp, x, g, pixel, s1, rng, acc, cnt);
+        if (go) {                    // one camera ray per lane: its next path's, or the one after
+            const bool now = L.state == SM_CAM && L.s < s1;
+            const bool pre = prefetch && L.state == SM_CAST && pf_s < 0 && L.s + 1 < s1;
+            if (now && !prefetch) {
+                L.start(kp, x, g, pixel, s1, rng, acc, cnt);
+            } else if (now || pre) {
+                const int cs = now ? L.s : L.s + 1;
+                CamDraws w{philox4x32_10(0u, 0u, pixel, (uint32_t)(kp.s_base + cs), kp.key0, kp.key1), 0};
+                V3 no, rd;
+                camera_ray<false>(kp, x, g, w, no, rd);
+                if (now) {
+                    L.begin(kp, pixel, no, rd, rng, acc, cnt);
+                } else {
+                    lds_put(pf, 0, no);
+                    lds_put(pf, 3, rd);
+                    pf_s = cs;
+                }
+            }
+        }
         if (L.state == SM_CAST) {
             L.cast_flat(kp, cnt);
             L.resolve(kp, acc, cnt);

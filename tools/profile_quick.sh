@@ -1,0 +1,8 @@
+#!/bin/bash
+# One kernel-trace pass and one SQ PMC pass of bench.py (C2) -> gpurun_out/$1
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-pq}
+mkdir -p $OUT
+B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- $B > $OUT/kt.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/sq -o run --output-format csv -- $B > $OUT/sq.log 2>&1
