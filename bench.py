@@ -205,6 +205,14 @@ def main():
     launch_samples = px_local * SPP
     flops = flops_per_launch(cnt, len(spheres), 0) * (launch_samples / max(cnt[0], 1))
     achieved_tflops = flops / (kernel_ms * 1e-3) / 1e12
+    # the reference's own work (no zero-throughput exit: every path runs its
+    # bounces) at the same rate: what the frame costs main.c's algorithm
+    d_ref = torch.zeros(tipe_rt.RT_NCOUNTERS, dtype=torch.int64, device=dev)
+    with tipe_rt.reference_counts():
+        tipe_rt.count_async(ds, p_cnt, tiling, d_ref.data_ptr(), sptr)
+        torch.cuda.synchronize(dev)
+    cnt_ref = [int(x) for x in d_ref.cpu()]
+    flops_ref = flops_per_launch(cnt_ref, len(spheres), 0) * (launch_samples / max(cnt_ref[0], 1))
     out_bytes = px_local * 3 * 24
     traffic = load_pmc_traffic()
 
@@ -226,9 +234,15 @@ def main():
                        "arith": "fp64, reference op order (bit-exact vs oracle)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP64_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / FP64_VECTOR_PEAK_TFLOPS, 4),
-                         "traffic": traffic, "kernel": "render_kernel<false, false, false>",
+                         "traffic": traffic, "kernel": "render_kernel_q<false> (persistent task queue) + combine_kernel",
                          "kernel_ms": round(kernel_ms, 3), "flops_per_launch": flops,
                          "flops_per_sample": round(flops / launch_samples, 1),
+                         "note": "achieved = algorithmic FLOPs of the work done (SURVEY 8d formula on the "
+                                 "kernel's own event counts; paths end at zero throughput) / kernel time",
+                         "reference_work": {"flops_per_sample": round(flops_ref / launch_samples, 1),
+                                            "tflops_equivalent": round(flops_ref / (kernel_ms * 1e-3) / 1e12, 3),
+                                            "frac": round(flops_ref / (kernel_ms * 1e-3) / 1e12
+                                                          / FP64_VECTOR_PEAK_TFLOPS, 4)},
                          "hbm": {"achieved_GBps": round(out_bytes / (kernel_ms * 1e-3) / 1e9, 4),
                                  "peak_GBps": HBM_PEAK_GBS,
                                  "frac": out_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,

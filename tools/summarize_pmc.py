@@ -10,14 +10,15 @@ os.makedirs(dst, exist_ok=True)
 def rows(d):
     p = os.path.join(src, d, "run_counter_collection.csv")
     return list(csv.DictReader(open(p))) if os.path.exists(p) else []
-def per_dispatch(d, counter, kname="render_kernel<false, false, false>"):
+KNAME = os.environ.get("KNAME", "render_kernel_q<false>")      # the C2 hot kernel (was render_kernel<false, false, false>)
+def per_dispatch(d, counter, kname=KNAME):
     acc = {}
     for r in rows(d):
         if kname in r["Kernel_Name"] and r["Counter_Name"] == counter:
             acc[r["Dispatch_Id"]] = acc.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return statistics.mean(acc.values()) if acc else None
 ks = list(csv.DictReader(open(os.path.join(src, "kt", "run_kernel_stats.csv"))))
-render = [k for k in ks if "render_kernel<false, false, false>" in k["Name"]][0]
+render = [k for k in ks if KNAME in k["Name"]][0]
 fetch_kib = per_dispatch("fetch", "FETCH_SIZE")
 write_kib = per_dispatch("write", "WRITE_SIZE")
 hbm = (2 * fetch_kib + write_kib) * 1024 if fetch_kib is not None else None
@@ -49,7 +50,7 @@ out = {"kernel": render["Name"], "calls": int(render["Calls"]), "avg_ms": dur_ns
                           / (dur_ns * 1e-9) / 1e12
                           if fl["SQ_INSTS_VALU_FLOPS_FP64"] and fl["SQ_ACTIVE_INST_VALU"] else None),
        "note": "FETCH_SIZE doubled (gfx950 reports half of wide-load bytes, MI355X_MICROARCH.md HBM); "
-               "units KiB; per render_kernel<false, false, false> launch; PMC runs are separate rocprofv3 passes"}
+               "units KiB; per " + KNAME + " launch; PMC runs are separate rocprofv3 passes"}
 json.dump(out, open(os.path.join(dst, "summary.json"), "w"), indent=1)
 for f in ["kt/run_kernel_stats.csv"]:
     os.system("cp %s %s" % (os.path.join(src, f), os.path.join(dst, "kernel_stats.csv")))
