@@ -84,6 +84,10 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_QUEUE                    // sphere kernel, spp_chunks > 1: persistent lanes + (chunk, pixel) task queue
 #define RT_QUEUE 64                 // (tasks per atomic grab of a wave; 0: off)
 #endif
+static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) must fit one batch");
+#ifndef RT_WAVES_PER_SIMD_Q         // queue kernel occupancy bound
+#define RT_WAVES_PER_SIMD_Q RT_WAVES_PER_SIMD
+#endif
 #ifndef RT_PREFETCH                 // queue kernel: camera rays computed one path ahead (LDS)
 #define RT_PREFETCH 1
 #endif
@@ -1741,7 +1745,7 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
 // the resident capacity; every lane leaves once the counter passes the
 // task count.
 template <bool SKY>
-__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD) void render_kernel_q(const KParams kp)
+__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
 {
     __shared__ double acc_lds[ACC_INC * 256];
     __shared__ double pf_lds[(RT_PREFETCH ? 6 : 1) * 256];   // a camera ray computed ahead (o, d)
