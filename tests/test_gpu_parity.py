@@ -194,6 +194,15 @@ def test_task_queue_kernel_bitexact(case, monkeypatch):
     check_parity(bundle, p)
 
 
+@pytest.mark.parametrize("B,W,H,S,P", [(0, 16, 12, 4, 2), (1, 16, 12, 6, 3), (2, 1, 1, 8, 4), (6, 1, 7, 5, 5),
+                                        (6, 9, 1, 4, 4)])
+def test_task_queue_kernel_edges(B, W, H, S, P):
+    """Queue kernel edge cases: no bounce (tracer's zero path, no camera-ray
+    prefetch), one bounce, 1-pixel / 1-column / 1-row frames (main.c:265
+    divides by W-1 = 0), one sample per chunk."""
+    check_parity(helpers.cornell(), helpers.params(W, H, S, B, chunks=P))
+
+
 def test_task_queue_kernel_cyclic_tiles():
     """The queue kernel on a rank's cyclic row tiles (multi-GPU layout)."""
     import torch
