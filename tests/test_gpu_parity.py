@@ -203,6 +203,17 @@ def test_task_queue_kernel_edges(B, W, H, S, P):
     check_parity(helpers.cornell(), helpers.params(W, H, S, B, chunks=P))
 
 
+@pytest.mark.parametrize("ns,nt", [(32, 0), (128, 0), (32, 100), (10, 1000), (128, 1000)])
+def test_synthetic_sweep_scenes_bitexact(ns, nt):
+    """The roofline-sweep scenes (tools/roofline_sweep.py):
+    up to 128 spheres (the candidate pass over 64 scalar-loaded pairs) and
+    1000 random triangles (BVH), with the queue kernel (chunks) and without."""
+    sph, mesh = tipe_rt.scenes.synthetic_cornell(ns, nt)
+    bundle = helpers.SceneBundle(sph, mesh)
+    check_parity(bundle, helpers.params(32, 24, 4, 6, chunks=2))
+    check_parity(bundle, helpers.params(24, 18, 3, 5, use_ao=True, ao=2.5, compat=0))
+
+
 def test_task_queue_kernel_cyclic_tiles():
     """The queue kernel on a rank's cyclic row tiles (multi-GPU layout)."""
     import torch

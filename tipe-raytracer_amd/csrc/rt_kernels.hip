@@ -88,6 +88,9 @@ static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) m
 #ifndef RT_WAVES_PER_SIMD_Q         // queue kernel occupancy bound
 #define RT_WAVES_PER_SIMD_Q RT_WAVES_PER_SIMD
 #endif
+#ifndef RT_QUEUE_BVH                // queue kernel also for BVH scenes (each lane walks its own tree)
+#define RT_QUEUE_BVH 0
+#endif
 #ifndef RT_PREFETCH                 // queue kernel: camera rays computed one path ahead (LDS)
 #define RT_PREFETCH 1
 #endif
@@ -1296,10 +1299,12 @@ struct LanePath {
         }
     }
 
-    // the whole cast without a BVH (spheres + brute-force triangles)
+    // the whole cast in one go (spheres, then brute-force triangles or the
+    // lane's own BVH walk)
+    template <bool BVH = false>
     __device__ __forceinline__ void cast_flat(const KParams& kp, Cnt& cnt)
     {
-        kind = closest_hit<COUNT, false>(kp, o, cd, best, win, cnt);
+        kind = closest_hit<COUNT, BVH>(kp, o, cd, best, win, cnt);
         state = SM_RESOLVE;
     }
 
@@ -1744,8 +1749,8 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
 // atomic per lane grab was 1.8x slower (same-address atomics).  The grid is
 // the resident capacity; every lane leaves once the counter passes the
 // task count.
-template <bool SKY>
-__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
+template <bool SKY, bool BVH>
+__global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
 {
     __shared__ double acc_lds[ACC_INC * 256];
     __shared__ double pf_lds[(RT_PREFETCH ? 6 : 1) * 256];   // a camera ray computed ahead (o, d)
@@ -1848,7 +1853,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
             }
         }
         if (L.state == SM_CAST) {
-            L.cast_flat(kp, cnt);
+            L.template cast_flat<BVH>(kp, cnt);
             L.resolve(kp, acc, cnt);
         }
     }
@@ -2051,16 +2056,18 @@ static void launch_variant(const KParams& kp, void* stream)
 
 #if RT_QUEUE > 0
 // Resident blocks of the queue kernel on this device (grid of render_kernel_q).
-static unsigned queue_grid(bool sky)
+static unsigned queue_grid(bool sky, bool bvh)
 {
-    static int cached[2][64];
+    static int cached[4][64];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    int& c = cached[sky ? 1 : 0][dev & 63];
+    int& c = cached[(sky ? 1 : 0) + (bvh ? 2 : 0)][dev & 63];
     if (c <= 0) {
         int nb = 0, ncu = 0;
-        if (sky) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<true>, 256, 0);
-        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<false>, 256, 0);
+        if (bvh && sky) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<true, true>, 256, 0);
+        else if (bvh) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<false, true>, 256, 0);
+        else if (sky) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<true, false>, 256, 0);
+        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<false, false>, 256, 0);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         c = std::max(1, nb) * std::max(1, ncu);
         if (const char* e = std::getenv("RT_QUEUE_BLOCKS")) c = std::max(1, std::atoi(e));   // experiments
@@ -2073,18 +2080,21 @@ static unsigned queue_grid(bool sky)
 int launch_render(const KParams& kp, void* stream)
 {
 #if RT_QUEUE > 0
-    if (kp.task_ctr && kp.chunks > 1 && !kp.bvh && !kp.cuda && !kp.sums) {
+    if (kp.task_ctr && kp.chunks > 1 && (!kp.bvh || RT_QUEUE_BVH) && !kp.cuda && !kp.sums) {
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
-        const unsigned nb = queue_grid(sky);
+        const bool bvh = kp.bvh != nullptr;
+        const unsigned nb = queue_grid(sky, bvh);
         unsigned long long* tr = nullptr;
         const char* tf = std::getenv("RT_QUEUE_TRACE");
         if (tf) (void)hipMalloc((void**)&tr, (size_t)nb * 256 * 4 * sizeof(unsigned long long));
         KParams k2 = kp;
         k2.trace = tr;
-        if (sky) hipLaunchKernelGGL(render_kernel_q<true>, dim3(nb), dim3(256), 0, st, k2);
-        else hipLaunchKernelGGL(render_kernel_q<false>, dim3(nb), dim3(256), 0, st, k2);
+        if (bvh && sky) hipLaunchKernelGGL((render_kernel_q<true, true>), dim3(nb), dim3(256), 0, st, k2);
+        else if (bvh) hipLaunchKernelGGL((render_kernel_q<false, true>), dim3(nb), dim3(256), 0, st, k2);
+        else if (sky) hipLaunchKernelGGL((render_kernel_q<true, false>), dim3(nb), dim3(256), 0, st, k2);
+        else hipLaunchKernelGGL((render_kernel_q<false, false>), dim3(nb), dim3(256), 0, st, k2);
         if (tr) {
             std::vector<unsigned long long> h((size_t)nb * 256 * 4);
             (void)hipStreamSynchronize(st);

@@ -142,3 +142,44 @@ def with_cuda_materials(mesh):
     for k in range(len(tris)):
         tris[k].mat = mats[qm[k] * tw * th]
     return mesh
+
+
+def synthetic_cornell(n_spheres=10, n_tris=0, seed=7):
+    """SURVEY.md §8(d)'s roofline-sweep scenes: the README box with
+    n_spheres - 10 extra small spheres (70 % diffuse, 15 % mirror, 15 %
+    emitters) and n_tris small random triangles inside the box, textured by
+    one 2x2 material table (material 0: no texture.h overrides).  Returns
+    (spheres, mesh) with mesh = (triangles, quelMatPourTri, mat_list, tw,
+    th, n_materials) or None; deterministic in seed."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    extra = []
+    for _ in range(max(0, n_spheres - len(README_SPHERES))):
+        c = (rng.uniform(-0.9, 0.9), rng.uniform(-0.9, 0.9), rng.uniform(-3.5, -1.0))
+        r = rng.uniform(0.04, 0.12)
+        kind = rng.uniform()
+        col = tuple(rng.uniform(0.1, 1.0, 3))
+        if kind < 0.70:
+            m = material(col)
+        elif kind < 0.85:
+            m = material(col, BLACK, 0.0, 0.9)
+        else:
+            m = material(BLACK, col, rng.uniform(2.0, 4.0))
+        extra.append((c, r, m))
+    spheres = cornell_spheres(extra=extra)
+    if n_tris <= 0:
+        return spheres, None
+    tris = (Triangle * n_tris)()
+    qm = (C.c_int * n_tris)()
+    for k in range(n_tris):
+        ctr = np.array([rng.uniform(-0.9, 0.9), rng.uniform(-0.95, 0.9), rng.uniform(-3.5, -1.0)])
+        e1, e2 = rng.normal(size=3), rng.normal(size=3)
+        s = rng.uniform(0.05, 0.15)
+        A, B, Cv = ctr, ctr + s * e1 / np.linalg.norm(e1), ctr + s * e2 / np.linalg.norm(e2)
+        tris[k].A, tris[k].B, tris[k].C = Vec3(*A), Vec3(*B), Vec3(*Cv)
+        tris[k].uvA, tris[k].uvB, tris[k].uvC = (UV(*rng.uniform(0, 1, 2)) for _ in range(3))
+        qm[k] = 0
+    mats = (Material * 4)()
+    for i in range(4):
+        mats[i] = material(tuple(rng.uniform(0.2, 0.9, 3)))
+    return spheres, (tris, qm, mats, 2, 2, 1)

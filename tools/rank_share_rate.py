@@ -12,10 +12,11 @@ from tipe_rt import scenes
 ap = argparse.ArgumentParser()
 ap.add_argument("--spp", type=int, default=1000)
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--chunks", type=int, default=32)
 args = ap.parse_args()
 W, H = 1200, 900
 cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
-p = tipe_rt.make_params(W, H, args.spp, 6, cam, focus=3.0, seed=1010, chunks=32)
+p = tipe_rt.make_params(W, H, args.spp, 6, cam, focus=3.0, seed=1010, chunks=args.chunks)
 ds = tipe_rt.DeviceScene(tipe_rt.make_scene(scenes.cornell_spheres()), 0)
 st = torch.cuda.current_stream().cuda_stream
 base = None
@@ -34,6 +35,6 @@ for n in (1, 2, 4, 8):
                 if t.row_base + (t.tile_first + lt * t.tile_step) * t.tile_rows + y < H)
     rate = valid * W * args.spp / dt / 1e6
     base = base or rate
-    print(json.dumps({"n": n, "rows": valid, "ms": round(dt * 1e3, 3), "msamples_per_s_share": round(rate, 1),
+    print(json.dumps({"chunks": args.chunks, "n": n, "rows": valid, "ms": round(dt * 1e3, 3), "msamples_per_s_share": round(rate, 1),
                       "efficiency_vs_n1": round(rate / base, 4)}), flush=True)
 ds.close()
