@@ -175,7 +175,8 @@ def test_spp_chunks_row_bands(monkeypatch):
     check_parity(helpers.cornell(), helpers.params(37, 53, 8, 5, chunks=4))
 
 
-@pytest.mark.parametrize("case", ["cornell", "cornell_ao", "pyramid", "sky", "bands", "one_sample_chunks"])
+@pytest.mark.parametrize("case", ["cornell", "cornell_ao", "pyramid", "sky", "bands", "one_sample_chunks", "aperture",
+                                  "neg_zero_origin"])
 def test_task_queue_kernel_bitexact(case, monkeypatch):
     """spp_chunks > 1 without a BVH runs render_kernel_q: persistent lanes
     take (chunk, pixel) tasks from a counter in whatever order the waves get
@@ -188,6 +189,13 @@ def test_task_queue_kernel_bitexact(case, monkeypatch):
         "sky": lambda: (helpers.sky_scene(), helpers.params(48, 36, 9, 5, sky_mode=1, chunks=3)),
         "bands": lambda: (helpers.cornell(), helpers.params(37, 53, 8, 5, chunks=4)),
         "one_sample_chunks": lambda: (helpers.cornell(), helpers.params(33, 25, 5, 6, chunks=5)),
+        # aperture: rays leave from co + (dx, dy, 0), one camera ray kept ahead (not two)
+        "aperture": lambda: (helpers.cornell(), helpers.params(40, 30, 12, 5, aperture=(0.3, 0.2), compat=0,
+                                                              focus=2.5, chunks=3)),
+        # a -0 camera coordinate: co + (+0) would be +0, so also one ray ahead
+        "neg_zero_origin": lambda: (helpers.cornell(), helpers.params(
+            40, 30, 12, 5, chunks=3, cam=tipe_rt.init_camera((-0.0, 0.3, 0.5), (0.0, -0.5, -3.0), (0, 1, 0),
+                                                             70.0, 4.0 / 3.0))),
     }[case]()
     if case == "bands":
         monkeypatch.setenv("RT_PARTIAL_BUDGET", str(16 * 37 * 4 * 72))

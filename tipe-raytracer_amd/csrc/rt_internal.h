@@ -102,6 +102,7 @@ struct KParams {
     double* partial;         // chunks > 1: [chunks][band_rows*W][9]
     double* sums;            // accumulate mode (rt_accumulate_async): [local_rows*W][9] running sums, or null
     long long s_base;        // global index of this launch's first sample (Philox counter word 3)
+    int pf_two;              // queue kernel may keep two camera directions ahead (rays start exactly at the camera origin)
     unsigned* task_ctr;      // render_kernel_q's task counter (zeroed per band launch), or null
     unsigned long long* trace;   // render_kernel_q diagnostics (RT_QUEUE_TRACE), normally null
     unsigned long long* counters;

@@ -88,6 +88,9 @@ static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) m
 #ifndef RT_WAVES_PER_SIMD_Q         // queue kernel occupancy bound
 #define RT_WAVES_PER_SIMD_Q RT_WAVES_PER_SIMD
 #endif
+#ifndef RT_PF_DEPTH                 // queue kernel: camera rays ahead per lane (2 needs no aperture)
+#define RT_PF_DEPTH 1               // (2 measured -2 % at fill 4, equal at fill 3: events are not the limit)
+#endif
 #ifndef RT_QUEUE_BVH                // queue kernel also for BVH scenes (each lane walks its own tree)
 #define RT_QUEUE_BVH 0
 #endif
@@ -1772,17 +1775,30 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
     bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
     const long long t_start = kp.trace ? wall_clock64() : 0;
     unsigned rounds = 0, ntasks = 0;
-    int pf_s = -1;                   // sample whose camera ray waits in pf (this task), or -1
+    // Camera rays computed ahead live in pf: with kp.pf_two (no aperture, so
+    // every ray starts exactly at the camera origin) up to two directions, of
+    // samples s+1 and s+2 in slots (s & 1); otherwise one ray (o, d).
+    // pf_hi: the last sample of the task whose ray is computed (in flight or
+    // in pf).
+    int pf_hi = -1;
     double* pf = pf_lds + threadIdx.x;
     const bool prefetch = RT_PREFETCH && kp.B > 0;
+    const int depth = (RT_PF_DEPTH >= 2 && kp.pf_two) ? 2 : 1;
     while (L.state != SM_DONE) {
         ++rounds;
-        if (L.state == SM_CAM && pf_s == L.s) {     // path done, next sample's ray is ready
-            L.begin(kp, pixel, lds_get(pf, 0), lds_get(pf, 3), rng, acc, cnt);
-            pf_s = -1;
+        if (L.state == SM_CAM && L.s < s1 && pf_hi >= L.s) {    // path done, next sample's ray is ready
+            if (depth == 2) {
+                const cdptr U = (cdptr)kp.uni;
+                const int b = opq0();
+                L.begin(kp, pixel, v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]),
+                        lds_get(pf, 3 * (L.s & 1)), rng, acc, cnt);
+            } else {
+                L.begin(kp, pixel, lds_get(pf, 0), lds_get(pf, 3), rng, acc, cnt);
+            }
         }
         const unsigned long long live = __ballot(1), wait = __ballot(L.state == SM_CAM);
-        const unsigned long long lack = __ballot(prefetch && L.state == SM_CAST && pf_s < 0 && L.s + 1 < s1);
+        // lanes with no ray ready for their next path
+        const unsigned long long lack = __ballot(prefetch && L.state == SM_CAST && pf_hi <= L.s && L.s + 1 < s1);
         const bool go = wait == live || (__popcll(wait) + __popcll(lack)) * 8 >= __popcll(live) * RT_QUEUE_FILL;
         const bool need = go && L.state == SM_CAM && L.s >= s1;
         const unsigned long long nm = __ballot(need);
@@ -1830,25 +1846,28 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
 #pragma unroll
                     for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
                     owns = true;
+                    pf_hi = L.s - 1;
                 }
             }
         }
-        if (go) {                    // one camera ray per lane: its next path's, or the one after
+        if (go) {                    // one camera ray per lane: its next path's, or one ahead
             const bool now = L.state == SM_CAM && L.s < s1;
-            const bool pre = prefetch && L.state == SM_CAST && pf_s < 0 && L.s + 1 < s1;
+            const bool pre = prefetch && L.state == SM_CAST && pf_hi < min(L.s + depth, s1 - 1);
             if (now && !prefetch) {
                 L.start(kp, x, g, pixel, s1, rng, acc, cnt);
             } else if (now || pre) {
-                const int cs = now ? L.s : L.s + 1;
+                const int cs = now ? L.s : pf_hi + 1;
                 CamDraws w{philox4x32_10(0u, 0u, pixel, (uint32_t)(kp.s_base + cs), kp.key0, kp.key1), 0};
                 V3 no, rd;
                 camera_ray<false>(kp, x, g, w, no, rd);
+                pf_hi = cs;
                 if (now) {
                     L.begin(kp, pixel, no, rd, rng, acc, cnt);
+                } else if (depth == 2) {
+                    lds_put(pf, 3 * (cs & 1), rd);
                 } else {
                     lds_put(pf, 0, no);
                     lds_put(pf, 3, rd);
-                    pf_s = cs;
                 }
             }
         }
