@@ -17,14 +17,18 @@ from tipe_rt import scenes
 ap = argparse.ArgumentParser()
 ap.add_argument("--spp", type=int, default=64)
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--only", default="", help="Ns:Nt[,Ns:Nt...] subset")
 args = ap.parse_args()
 W, H, B = 1200, 900, 6
 PEAK = 78.6
 cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
 st = torch.cuda.current_stream().cuda_stream
 T = tipe_rt.types
-for ns in (10, 32, 128):
-    for nt in (0, 100, 1000):
+grid = [(ns, nt) for ns in (10, 32, 128) for nt in (0, 100, 1000)]
+if args.only:
+    grid = [tuple(int(v) for v in x.split(":")) for x in args.only.split(",")]
+for ns, nt in grid:
+    if True:
         sph, mesh = scenes.synthetic_cornell(ns, nt)
         scene = tipe_rt.make_scene(sph, *mesh) if mesh else tipe_rt.make_scene(sph)
         ds = tipe_rt.DeviceScene(scene, 0)
