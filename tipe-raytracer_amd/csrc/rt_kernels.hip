@@ -88,6 +88,9 @@ static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) m
 #ifndef RT_WAVES_PER_SIMD_Q         // queue kernel occupancy bound
 #define RT_WAVES_PER_SIMD_Q RT_WAVES_PER_SIMD
 #endif
+#ifndef RT_QUEUE_WAIT               // ... or once this many eighths of the lanes wait with no ray (9: never)
+#define RT_QUEUE_WAIT 9
+#endif
 #ifndef RT_PF_DEPTH                 // queue kernel: camera rays ahead per lane (2 needs no aperture)
 #define RT_PF_DEPTH 1               // (2 measured -2 % at fill 4, equal at fill 3: events are not the limit)
 #endif
@@ -1799,7 +1802,8 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
         const unsigned long long live = __ballot(1), wait = __ballot(L.state == SM_CAM);
         // lanes with no ray ready for their next path
         const unsigned long long lack = __ballot(prefetch && L.state == SM_CAST && pf_hi <= L.s && L.s + 1 < s1);
-        const bool go = wait == live || (__popcll(wait) + __popcll(lack)) * 8 >= __popcll(live) * RT_QUEUE_FILL;
+        const bool go = wait == live || (__popcll(wait) + __popcll(lack)) * 8 >= __popcll(live) * RT_QUEUE_FILL ||
+                        __popcll(wait) * 8 >= __popcll(live) * RT_QUEUE_WAIT;
         const bool need = go && L.state == SM_CAM && L.s >= s1;
         const unsigned long long nm = __ballot(need);
         unsigned t = 0;
