@@ -234,7 +234,7 @@ def main():
                        "arith": "fp64, reference op order (bit-exact vs oracle)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP64_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / FP64_VECTOR_PEAK_TFLOPS, 4),
-                         "traffic": traffic, "kernel": "render_kernel_q<false> (persistent task queue) + combine_kernel",
+                         "traffic": traffic, "kernel": "render_kernel_q<false, false> (persistent task queue) + combine_kernel",
                          "kernel_ms": round(kernel_ms, 3), "flops_per_launch": flops,
                          "flops_per_sample": round(flops / launch_samples, 1),
                          "note": "achieved = algorithmic FLOPs of the work done (SURVEY 8d formula on the "
