@@ -102,6 +102,8 @@ def main():
                          "for every N, so the image does not depend on the GPU count)")
     ap.add_argument("--verify", action="store_true",
                     help="N>1: rank 0 re-renders the frame alone and checks the assembled planes bit for bit")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="one stream: frame k+1 starts after frame k (default: two streams, see step())")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: gather through host copies (rehearsing N>1 with all ranks on one GPU); "
                          "nccl (= RCCL) is the measured configuration")
@@ -130,40 +132,52 @@ def main():
     else:
         tiling = tipe_rt.cyclic_tiling(H, TILE_ROWS, rank, world)
     rows = tiling.n_tiles * tiling.tile_rows
+    # Frames alternate between two streams with their own buffers, so frame
+    # k+1's persistent render blocks start on the CUs that frame k's last
+    # tasks leave idle (the queue kernel's tail); stream order
+    # keeps frame k+2 behind frame k's gather and assembly.
+    nbuf = 1 if args.no_pipeline else 2
+    streams = [stream] if nbuf == 1 else [torch.cuda.Stream(dev) for _ in range(nbuf)]
     # frame planes: canva | albedo | normal (the reference's three outputs)
-    local = torch.empty((3, rows, W, 3), dtype=torch.float64, device=dev)
-    gathered = gather_list = full = None
+    locals_ = [torch.empty((3, rows, W, 3), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+    gathered_ = gather_lists = fulls = [None] * nbuf
     if world > 1 and rank == 0:
-        gathered = torch.empty((world, 3, rows, W, 3), dtype=torch.float64, device=dev)
-        gather_list = [gathered[r] for r in range(world)]
-        full = torch.empty((3, H, W, 3), dtype=torch.float64, device=dev)
+        gathered_ = [torch.empty((world, 3, rows, W, 3), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+        gather_lists = [[g[r] for r in range(world)] for g in gathered_]
+        fulls = [torch.empty((3, H, W, 3), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+    last = [0]
 
-    def step():
-        tipe_rt.render_async(ds, p, tiling, local[0].data_ptr(), local[1].data_ptr(), local[2].data_ptr(),
-                             None, sptr)
-        if world > 1:
-            if args.dist_backend == "nccl":
-                dist.gather(local, gather_list, dst=0)     # RCCL over xGMI
-            else:
-                host = [torch.empty_like(local, device="cpu") for _ in range(world)] if rank == 0 else None
-                dist.gather(local.cpu(), host, dst=0)
+    def step(k):
+        b = k % nbuf
+        last[0] = b
+        st = streams[b]
+        local, gathered, gather_list, full = locals_[b], gathered_[b], gather_lists[b], fulls[b]
+        with torch.cuda.stream(st):
+            tipe_rt.render_async(ds, p, tiling, local[0].data_ptr(), local[1].data_ptr(), local[2].data_ptr(),
+                                 None, st.cuda_stream)
+            if world > 1:
+                if args.dist_backend == "nccl":
+                    dist.gather(local, gather_list, dst=0)     # RCCL over xGMI
+                else:
+                    host = [torch.empty_like(local, device="cpu") for _ in range(world)] if rank == 0 else None
+                    dist.gather(local.cpu(), host, dst=0)
+                    if rank == 0:
+                        for r in range(world):
+                            gathered[r].copy_(host[r])
                 if rank == 0:
-                    for r in range(world):
-                        gathered[r].copy_(host[r])
-            if rank == 0:
-                for pl in range(3):                     # (world, plane, rows, W, 3) -> (plane, H, W, 3)
-                    tipe_rt.assemble_async(gathered[0, pl].data_ptr(), world, TILE_ROWS, rows, W, H,
-                                           full[pl].data_ptr(), sptr, rank_stride=3 * rows * W)
+                    for pl in range(3):                     # (world, plane, rows, W, 3) -> (plane, H, W, 3)
+                        tipe_rt.assemble_async(gathered[0, pl].data_ptr(), world, TILE_ROWS, rows, W, H,
+                                               full[pl].data_ptr(), st.cuda_stream, rank_stride=3 * rows * W)
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(k)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        step(k)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -180,13 +194,15 @@ def main():
         tipe_rt.render_async(ds, p, tipe_rt.band_tiling(0, H - 1), ref[0].data_ptr(), ref[1].data_ptr(),
                              ref[2].data_ptr(), None, sptr)
         torch.cuda.synchronize(dev)
-        verified = bool(torch.equal(ref, full))
+        used = fulls[:min(nbuf, args.warmup + args.steps)]            # every buffer that held a frame
+        verified = all(bool(torch.equal(ref, f)) for f in used)
         if not verified:
             print("verify: assembled frame differs from the single-device frame", file=sys.stderr)
 
     # --- kernel-only timing with HIP events on the launch stream ------------
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     n_k = max(1, min(args.steps, 3))
+    local = locals_[0]
     ev[0].record(stream)
     for _ in range(n_k):
         tipe_rt.render_async(ds, p, tiling, local[0].data_ptr(), local[1].data_ptr(), local[2].data_ptr(),
@@ -227,7 +243,7 @@ def main():
             "data": "synthetic scene: README 10-sphere Cornell box (alpha=1, materialIndex=1), Philox seed 1010",
             "config": {"workload": "C2: 10-sphere Cornell box, 1200x900, 1000 spp, 6 bounces",
                        "width": W, "height": H, "spp": SPP, "bounces": BOUNCES,
-                       "tile_rows": TILE_ROWS if world > 1 else H, "parallelism": "row-tiles x%d" % world,
+                       "tile_rows": TILE_ROWS if world > 1 else H, "parallelism": "row-tiles x%d" % world, "frames_in_flight": nbuf,
                        "collective": ("rccl gather" if args.dist_backend == "nccl" else "gloo gather (host)")
                        if world > 1 else None,
                        "rng": "philox4x32-10", "spp_chunks": args.chunks,

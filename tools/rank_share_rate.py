@@ -13,6 +13,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--spp", type=int, default=1000)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--chunks", type=int, default=32)
+ap.add_argument("--pipeline", action="store_true", help="alternate two streams (bench.py default)")
 args = ap.parse_args()
 W, H = 1200, 900
 cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
@@ -23,18 +24,23 @@ base = None
 for n in (1, 2, 4, 8):
     t = tipe_rt.band_tiling(0, H - 1) if n == 1 else tipe_rt.cyclic_tiling(H, 2, 0, n)
     rows = t.n_tiles * t.tile_rows
-    out = torch.empty((3, rows, W, 3), dtype=torch.float64, device="cuda:0")
-    tipe_rt.render_async(ds, p, t, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), None, st)
+    nb = 2 if args.pipeline else 1
+    outs = [torch.empty((3, rows, W, 3), dtype=torch.float64, device="cuda:0") for _ in range(nb)]
+    sts = [torch.cuda.Stream() for _ in range(nb)] if args.pipeline else [torch.cuda.current_stream()]
+    def frame(k):
+        o, s_ = outs[k % nb], sts[k % nb]
+        tipe_rt.render_async(ds, p, t, o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(), None, s_.cuda_stream)
+    frame(0)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.reps):
-        tipe_rt.render_async(ds, p, t, out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(), None, st)
+    for k in range(args.reps):
+        frame(k)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.reps
     valid = sum(1 for lt in range(t.n_tiles) for y in range(t.tile_rows)
                 if t.row_base + (t.tile_first + lt * t.tile_step) * t.tile_rows + y < H)
     rate = valid * W * args.spp / dt / 1e6
     base = base or rate
-    print(json.dumps({"chunks": args.chunks, "n": n, "rows": valid, "ms": round(dt * 1e3, 3), "msamples_per_s_share": round(rate, 1),
+    print(json.dumps({"chunks": args.chunks, "pipeline": args.pipeline, "n": n, "rows": valid, "ms": round(dt * 1e3, 3), "msamples_per_s_share": round(rate, 1),
                       "efficiency_vs_n1": round(rate / base, 4)}), flush=True)
 ds.close()
