@@ -21,7 +21,15 @@ from test_gpu_parity import check_parity
 pytestmark = pytest.mark.gpu
 
 
-def random_scene(seed):
+def _zero_some(rng, c, zeros):
+    """With zeros, each colour channel is exactly 0 with probability 0.35,
+    so rayColor reaches (0, 0, 0) and the zero-throughput exit runs."""
+    if not zeros:
+        return c
+    return tuple(0.0 if rng.random() < 0.35 else float(x) for x in c)
+
+
+def random_scene(seed, zeros=False, chunks=None):
     rng = np.random.default_rng(seed)
     ns = int(rng.integers(1, 14))
     sph = (Sphere * ns)()
@@ -29,7 +37,7 @@ def random_scene(seed):
         kind = rng.choice(["diffuse", "mirror", "glass", "hole", "light", "big"])
         c = rng.uniform([-2, -2, -6], [2, 2, -1])
         r = rng.uniform(0.2, 1.2)
-        diff = tuple(rng.uniform(0, 1, 3))
+        diff = _zero_some(rng, tuple(rng.uniform(0, 1, 3)), zeros)
         em, es, refl, alpha, ior = (0, 0, 0), 0.0, 0.0, 1.0, 1.0
         if kind == "mirror":
             refl = float(rng.uniform(0.5, 1.0))
@@ -57,7 +65,7 @@ def random_scene(seed):
             tris[k].uvA, tris[k].uvB, tris[k].uvC = (UV(*rng.uniform(-2, 2, 2)) for _ in range(3))
         mats = (Material * (nm * tw * th))()
         for k in range(nm * tw * th):
-            mats[k] = scenes.material(tuple(rng.uniform(0, 1, 3)), (0, 0, 0), 0.0, 0.0,
+            mats[k] = scenes.material(_zero_some(rng, tuple(rng.uniform(0, 1, 3)), zeros), (0, 0, 0), 0.0, 0.0,
                                       float(rng.choice([0.0, 0.5, 1.0, 0.7])), 0.0)
         mesh = (tris, qm, mats, tw, th, nm)
     bundle = helpers.SceneBundle(sph, mesh)
@@ -68,12 +76,25 @@ def random_scene(seed):
                        ao=float(rng.uniform(0.5, 3.5)), seed=int(rng.integers(0, 2 ** 40)), cam=cam,
                        aperture=tuple(rng.choice([0.0, 0.0, 1.0, 2.0], 2)), focus=float(rng.uniform(1, 5)),
                        compat=int(rng.integers(0, 2)), chunks=int(rng.choice([1, 1, 2, 3])))
+    if chunks is not None:
+        p.spp_chunks = chunks
+        p.nbRayonParPixel = max(p.nbRayonParPixel, chunks)
     return bundle, p
 
 
 @pytest.mark.parametrize("seed", range(64))
 def test_random_scene_bitexact(seed):
     bundle, p = random_scene(seed)
+    check_parity(bundle, p)
+
+
+@pytest.mark.parametrize("seed", range(200, 248))
+def test_random_scene_zero_throughput_queue_bitexact(seed):
+    """Random scenes whose colours have exact-zero channels (paths end at
+    zero throughput), rendered with spp_chunks 2-4 (the queue kernel for
+    sphere/brute-force scenes, the BVH kernel on odd seeds), bit for bit
+    against the oracle, which never ends a path early."""
+    bundle, p = random_scene(seed, zeros=True, chunks=2 + seed % 3)
     check_parity(bundle, p)
 
 
