@@ -39,6 +39,7 @@
 //    in chunk order by combine_kernel (a deterministic, GPU-count-independent
 //    grouping that the oracle reproduces).
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -2079,12 +2080,16 @@ static void launch_variant(const KParams& kp, void* stream)
 
 #if RT_QUEUE > 0
 // Resident blocks of the queue kernel on this device (grid of render_kernel_q).
+// Cached per device and variant; rt_fill_canva may run on several host
+// threads at once (main.c's pthreads), so the cache is atomic (every thread
+// computes the same value).
 static unsigned queue_grid(bool sky, bool bvh)
 {
-    static int cached[4][64];
+    static std::atomic<int> cached[4][64];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    int& c = cached[(sky ? 1 : 0) + (bvh ? 2 : 0)][dev & 63];
+    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (bvh ? 2 : 0)][dev & 63];
+    int c = slot.load(std::memory_order_relaxed);
     if (c <= 0) {
         int nb = 0, ncu = 0;
         if (bvh && sky) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<true, true>, 256, 0);
@@ -2095,6 +2100,7 @@ static unsigned queue_grid(bool sky, bool bvh)
         c = std::max(1, nb) * std::max(1, ncu);
         if (const char* e = std::getenv("RT_QUEUE_BLOCKS")) c = std::max(1, std::atoi(e));   // experiments
         if (std::getenv("RT_QUEUE_VERBOSE")) std::fprintf(stderr, "render_kernel_q: %d blocks/CU x %d CUs -> %d\n", nb, ncu, c);
+        slot.store(c, std::memory_order_relaxed);
     }
     return (unsigned)c;
 }
