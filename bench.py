@@ -11,7 +11,13 @@ tiles, the tiles are gathered to rank 0 over RCCL (torch.distributed.gather,
 backend "nccl") and rank 0 un-permutes them (rt_assemble_async): total work
 per step is fixed, so scaling is "strong".
 
-Rank 0 prints ONE JSON line.  `roofline` prices the render kernel against
+Rank 0 prints ONE JSON line.  Besides the C2 headline it carries (N = 1,
+rank 0): `configs` (C3, C4, C5 and the 10-sphere/100-triangle sweep scene at
+reduced spp, kernel rates and roofline fractions), `end_to_end` (host-buffer
+rates of the drop-ins rt_render_rows and rt_fill_canva x 12 pthreads, i.e.
+upload -> render -> assembled host framebuffer) and `cpu_baseline` with six
+legs (1, 12 and the box's CPU share of threads x faithful / fair RNG).
+`roofline` prices the render kernel against
 the FP64 vector peak: algorithmic FLOPs per launch = the per-sample formula
 of SURVEY.md §8(d) evaluated on event counts from rt_count_async (a counting
 pass outside the timed region), divided by the kernel's mean duration from
@@ -57,37 +63,221 @@ def valid_rows(t):
 
 
 def load_pmc_traffic():
-    """HBM bytes per render launch from the committed rocprofv3 --pmc pass, or None."""
+    """HBM bytes per render launch from the committed rocprofv3 --pmc pass
+    (profiles/pmc_traffic.json: value, profile directory, commit), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("render_kernel_hbm_bytes_per_launch")
+        return d.get("render_kernel_hbm_bytes_per_launch"), {k: v for k, v in d.items()
+                                                             if k != "render_kernel_hbm_bytes_per_launch"}
+    except Exception:
+        return None, None
+
+
+def cpu_share():
+    """CPUs this process may use: the cgroup quota (cpu.max) if any, else the affinity mask."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except Exception:
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def cpu_smt():
+    try:
+        return int(open("/sys/devices/system/cpu/smt/active").read().strip()) == 1
     except Exception:
         return None
 
 
-def cpu_baseline(p, scene_bundle, threads=12):
-    """Oracle (CPU restatement, Philox stream = per-pixel, i.e. the 'fair'
-    per-thread RNG) with `threads` pthreads on 5 bands of `threads` rows of
-    the C2 frame at the full 1000 spp."""
+def cpu_baseline(scene, cam, threads=12):
+    """The CPU restatement (oracle/rt_oracle.c) on the full C2 frame at
+    reduced spp, main.c's partition (NUM_THREADS contiguous row bands,
+    main.c:407-449), in six legs: NUM_THREADS in {1, `threads`, the box's
+    CPU share} x RNG mode
+      faithful: one global glibc rand() stream shared by every thread, as
+                main.c's threads share it (lock-serialised; libm math);
+      fair:     a lock-free stream per pixel (Philox; portable math).
+    Msamples/s does not depend on spp (pixels are independent), so each leg
+    renders the 1200x900 frame at 1-8 spp (about 1-14 s each on the GPU
+    box's 16-CPU share).  The headline is fair x 12."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi
     o = oracle_ffi.oracle()
     canva = np.zeros((H, W, 3))
-    starts = [100, 250, 400, 550, 700, 850]
-    t0 = time.perf_counter()
-    for lo in starts:
-        rc = o.oracle_render_rows(C.byref(scene_bundle), C.byref(p), lo + threads - 1, lo, threads, 0,
-                                  canva.ctypes.data, None, None, None, None)
-        assert rc == 0
-    dt = time.perf_counter() - t0
-    samples = len(starts) * threads * W * SPP
-    return {"value": samples / dt / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": "%d bands x %d rows of the 1200x900 C2 frame at 1000 spp (%d samples, %.1f s), "
-                      "oracle/rt_oracle.c, Philox per-pixel stream, %d pthreads over contiguous row bands "
-                      "(main.c:407-449)" % (len(starts), threads, samples, dt, threads),
-            "host_nproc": os.cpu_count()}
+    share = cpu_share()
+    legs = {}
+    for mode, rng in (("fair", tipe_rt.RT_RNG_PHILOX), ("faithful", tipe_rt.RT_RNG_GLIBC)):
+        for nt in sorted({1, threads, share}):
+            spp = (8 if nt > 1 else 2) if mode == "fair" else (2 if nt == 1 else 1)
+            p = tipe_rt.make_params(W, H, spp, BOUNCES, cam, focus=3.0, seed=SEED, rng=rng, chunks=1)
+            t0 = time.perf_counter()
+            rc = o.oracle_render_rows(C.byref(scene), C.byref(p), H - 1, 0, nt, 1, canva.ctypes.data,
+                                      None, None, None, None)
+            dt = time.perf_counter() - t0
+            assert rc == 0
+            legs["%s_%dt" % (mode, nt)] = {"value": round(W * H * spp / dt / 1e6, 4), "threads": nt,
+                                            "spp": spp, "seconds": round(dt, 2)}
+    head = legs["fair_%dt" % threads]
+    return {"value": head["value"], "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": "full 1200x900 C2 frame at %d spp (other legs: see legs), oracle/rt_oracle.c (CPU restatement of main.c), "
+                      "%d pthreads over main.c's contiguous row bands (main.c:407-449), Philox per-pixel "
+                      "stream (the 'fair' leg; see legs)" % (head["spp"], threads),
+            "legs": legs, "cpu_model": cpu_model(), "smt": cpu_smt(), "host_logical_cpus": os.cpu_count(),
+            "cpu_share": share,
+            "note": "faithful = one lock-serialised glibc rand() stream shared by all threads (main.c's "
+                    "behaviour, rtutility.h:229-231); fair = lock-free per-pixel stream"}
+
+
+# ---- other BASELINE configs (kernel rates at reduced spp, N = 1) -------------
+CONFIGS = {
+    # name: (scene builder, spp measured, bounces, useAO, W, H, full spp, GPUs of the config)
+    "C3": ("pyramid", 100, 6, False, 1200, 900, 1000, 1),
+    "C4": ("tree", 32, 8, True, 1200, 900, 2000, 4),
+    "C5": ("pyramid", 20, 6, False, 3840, 2880, 5000, 8),
+    "sweep_10s_100t": ("sweep", 64, 6, False, 1200, 900, 64, 1),
+}
+
+
+def config_scene(kind):
+    sph = scenes.cornell_spheres()
+    if kind == "pyramid":
+        return tipe_rt.make_scene(sph, *scenes.pyramid_mesh()), len(sph), 5
+    if kind == "tree":
+        tris, qm, mats, tw, th, nm = scenes.tree_mesh()
+        return tipe_rt.make_scene(sph, tris, qm, mats, tw, th, nm), len(sph), len(tris)
+    sph, (tris, qm, mats, tw, th, nm) = scenes.synthetic_cornell(10, 100)
+    return tipe_rt.make_scene(sph, tris, qm, mats, tw, th, nm), len(sph), len(tris)
+
+
+def work_flops(c, ns):
+    """FLOPs of the work done per launch (roofline sweep convention):
+    SURVEY 8(d)'s terms with 40 per triangle test made and 48 per BVH node."""
+    T = tipe_rt.types
+    bvh = c[T.RT_CNT_BVH_NODES] > 0
+    tri_done = c[T.RT_CNT_BVH_TRI_TESTS] if bvh else c[T.RT_CNT_TRI_TESTS]
+    return (40 * c[0] + c[T.RT_CNT_CASTS] * (25 * ns + 18) + 40 * tri_done + 48 * c[T.RT_CNT_BVH_NODES]
+            + 5 * c[T.RT_CNT_SPHERE_DISC] + 100 * c[T.RT_CNT_SHADE] + 80 * c[T.RT_CNT_TEX_HITS]
+            + 40 * c[T.RT_CNT_REFRACT])
+
+
+def configs_extra(dev, stream, cam):
+    out = {}
+    sptr = stream.cuda_stream
+    for name, (kind, spp, bounces, ao, w, h, full_spp, gpus) in CONFIGS.items():
+        sc, ns, nt = config_scene(kind)
+        p = tipe_rt.make_params(w, h, spp, bounces, cam, focus=3.0, use_ao=ao, ao=2.5, seed=SEED,
+                                chunks=tipe_rt.RT_SPP_CHUNKS_AUTO)
+        ds = tipe_rt.DeviceScene(sc, dev.index)
+        tiling = tipe_rt.band_tiling(0, h - 1)
+        buf = torch.empty((3, h, w, 3), dtype=torch.float64, device=dev)
+
+        def launch():
+            tipe_rt.render_async(ds, p, tiling, buf[0].data_ptr(), buf[1].data_ptr(), buf[2].data_ptr(), None, sptr)
+        launch()
+        torch.cuda.synchronize(dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        reps = 2
+        ev[0].record(stream)
+        for _ in range(reps):
+            launch()
+        ev[1].record(stream)
+        torch.cuda.synchronize(dev)
+        ms = ev[0].elapsed_time(ev[1]) / reps
+        pc = tipe_rt.make_params(w, h, 2, bounces, cam, focus=3.0, use_ao=ao, ao=2.5, seed=SEED)
+        d = torch.zeros(tipe_rt.RT_NCOUNTERS, dtype=torch.int64, device=dev)
+        tipe_rt.count_async(ds, pc, tiling, d.data_ptr(), sptr)
+        torch.cuda.synchronize(dev)
+        c = [int(x) for x in d.cpu()]
+        ds.close()
+        rate = w * h * spp / (ms * 1e-3) / 1e6
+        fps = work_flops(c, ns) / max(c[0], 1)
+        tf = rate * 1e6 * fps / 1e12
+        T = tipe_rt.types
+        rec = {"kernel_msamples_per_s": round(rate, 1), "spp_measured": spp, "kernel_ms": round(ms, 3),
+               "width": w, "height": h, "bounces": bounces, "ao": ao, "spheres": ns, "triangles": nt,
+               "flops_per_sample_work_done": round(fps, 1), "achieved_tflops": round(tf, 3),
+               "frac": round(tf / FP64_VECTOR_PEAK_TFLOPS, 4),
+               "casts_per_sample": round(c[T.RT_CNT_CASTS] / max(c[0], 1), 3)}
+        if c[T.RT_CNT_BVH_NODES]:
+            rec["bvh_nodes_per_sample"] = round(c[T.RT_CNT_BVH_NODES] / c[0], 3)
+            rec["bvh_tri_tests_per_sample"] = round(c[T.RT_CNT_BVH_TRI_TESTS] / c[0], 3)
+            rec["bvh_simd_efficiency"] = round(c[T.RT_CNT_BVH_NODES] / max(c[T.RT_CNT_BVH_LANE_SLOTS], 1), 4)
+        if kind != "sweep":
+            rec["full_frame_s_at_config_spp_1gpu"] = round(w * h * full_spp / (rate * 1e6), 2)
+            rec["config_gpus"] = gpus
+        out[name] = rec
+    return out
+
+
+# ---- end-to-end host-buffer rates of the drop-ins (N = 1) --------------------
+def end_to_end(scene, spheres, cam, reps=2):
+    """Upload -> render -> assembled host framebuffer through the C-ABI:
+    rt_render_rows (one call, whole frame, canva + albedo + normal) and
+    rt_fill_canva on 12 threads over main.c's row bands (main.c:404-453).
+    Both use RT_SPP_CHUNKS_AUTO; the scene cache holds the upload after the
+    first (untimed) call, as it does for every frame after a program's first."""
+    import threading
+    from tipe_rt.types import ThreadData, Sphere
+    L = tipe_rt.lib()
+    p = tipe_rt.make_params(W, H, SPP, BOUNCES, cam, focus=3.0, seed=SEED, chunks=tipe_rt.RT_SPP_CHUNKS_AUTO)
+    canva, alb, nrm = (np.zeros((H, W, 3)) for _ in range(3))
+
+    def rows_call():
+        tipe_rt.check(L.rt_render_rows(C.byref(scene), C.byref(p), H - 1, 0, canva.ctypes.data, alb.ctypes.data,
+                                       nrm.ctypes.data))
+    NT = 12
+    rows = H // NT
+    tds = []
+    for t in range(NT):
+        hi = H - 1 - t * rows
+        td = ThreadData()
+        td.start_row, td.end_row = hi, (hi - rows + 1 if t < NT - 1 else 0)
+        td.canva = C.cast(canva.ctypes.data, C.POINTER(tipe_rt.Vec3))
+        td.albedo_tab = C.cast(alb.ctypes.data, C.POINTER(tipe_rt.Vec3))
+        td.normal_tab = C.cast(nrm.ctypes.data, C.POINTER(tipe_rt.Vec3))
+        td.cam = cam
+        td.largeur_image, td.hauteur_image = W, H
+        td.nbRayonParPixel, td.nbRebondMax = SPP, BOUNCES
+        td.total_pixels = W * H
+        td.sphere_list = C.cast(spheres, C.POINTER(Sphere))
+        td.nbSpheres = len(spheres)
+        td.focus_distance = 3
+        tds.append(td)
+
+    def fill_call():
+        res = []
+        ths = [threading.Thread(target=lambda t=t: res.append(L.rt_fill_canva(C.byref(t)))) for t in tds]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert all(r is None for r in res), L.rt_last_error()
+    out = {}
+    for name, fn in (("rt_render_rows", rows_call), ("rt_fill_canva_x12_pthreads", fill_call)):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        dt = (time.perf_counter() - t0) / reps
+        out[name] = {"msamples_per_s": round(W * H * SPP / dt / 1e6, 1), "ms_per_frame": round(dt * 1e3, 2)}
+    out["note"] = ("C2 frame, host buffers (canva, albedo, normal: 78 MB over PCIe), spp_chunks AUTO; "
+                   "the scene upload is cached after the first call; %d timed frames each" % reps)
+    return out
 
 
 def main():
@@ -96,6 +286,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the configs / end_to_end keys")
     ap.add_argument("--cpu-threads", type=int, default=12)
     ap.add_argument("--chunks", type=int, default=int(os.environ.get("RT_BENCH_CHUNKS", "32")),
                     help="rt_params.spp_chunks (fixed slice grouping of each pixel's samples; the same "
@@ -230,7 +421,12 @@ def main():
     cnt_ref = [int(x) for x in d_ref.cpu()]
     flops_ref = flops_per_launch(cnt_ref, len(spheres), 0) * (launch_samples / max(cnt_ref[0], 1))
     out_bytes = px_local * 3 * 24
-    traffic = load_pmc_traffic()
+    traffic, traffic_src = load_pmc_traffic()
+    # the render kernel's own writes by construction: one 72-B partial per
+    # (chunk, pixel) task (combine_kernel reads them back and writes the
+    # frame), or the frame itself with one chunk
+    chunks = tipe_rt.types.rt_resolve_spp_chunks(args.chunks, SPP)
+    traffic_model = px_local * 72 * chunks if chunks > 1 else out_bytes
 
     total_samples = W * H * SPP * args.steps
     value = total_samples / elapsed / 1e6
@@ -250,7 +446,8 @@ def main():
                        "arith": "fp64, reference op order (bit-exact vs oracle)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP64_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / FP64_VECTOR_PEAK_TFLOPS, 4),
-                         "traffic": traffic, "kernel": "render_kernel_q<false, false> (persistent task queue) + combine_kernel",
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_model_bytes_per_launch": traffic_model, "kernel": "render_kernel_q<false, false> (persistent task queue) + combine_kernel",
                          "kernel_ms": round(kernel_ms, 3), "flops_per_launch": flops,
                          "flops_per_sample": round(flops / launch_samples, 1),
                          "note": "achieved = algorithmic FLOPs of the work done (SURVEY 8d formula on the "
@@ -268,9 +465,11 @@ def main():
         }
         if verified is not None:
             rec["verified_vs_single_device"] = verified
+        if world == 1 and not args.no_extras:
+            rec["configs"] = configs_extra(dev, stream, cam)
+            rec["end_to_end"] = end_to_end(scene, spheres, cam)
         if world == 1 and not args.no_cpu_baseline:
-            pc = tipe_rt.make_params(W, H, SPP, BOUNCES, cam, focus=3.0, seed=SEED, chunks=args.chunks)
-            rec["cpu_baseline"] = cpu_baseline(pc, scene, threads=args.cpu_threads)
+            rec["cpu_baseline"] = cpu_baseline(scene, cam, threads=args.cpu_threads)
             rec["speedup_vs_cpu_baseline"] = round(value / rec["cpu_baseline"]["value"], 1)
         print(json.dumps(rec))
     ds.close()

@@ -78,7 +78,10 @@ typedef struct rt_params {
                                           then slice sums in slice order; a
                                           deterministic grouping (independent of
                                           GPU count) that lets one pixel's
-                                          samples run on P wavefronts          */
+                                          samples run on P wavefronts (the
+                                          persistent task-queue kernel).
+                                          RT_SPP_CHUNKS_AUTO: P = min(32, S),
+                                          see rt_resolve_spp_chunks          */
     unsigned long long seed;           /* Philox key                             */
     int accel;                         /* RT_ACCEL_*: triangle traversal          */
     int sky_mode;                      /* RT_SKY_*                                */
@@ -123,8 +126,24 @@ typedef struct rt_params {
 #define RT_ACCEL_AUTO 0
 #define RT_ACCEL_NONE 1
 
+/* rt_params.spp_chunks = RT_SPP_CHUNKS_AUTO selects the grouping the
+ * benchmarks use: P = min(RT_SPP_CHUNKS_DEFAULT, S) slices.  It depends only
+ * on S, so images are identical for any GPU count, tiling or thread count;
+ * the CPU oracle resolves it with the same function.  Against the strict
+ * sample order (P = 1) the grouping moves pre-gamma radiance by < 1e-12
+ * RMSE (floating-point re-association of the per-pixel sum). */
+#define RT_SPP_CHUNKS_AUTO    (-1)
+#define RT_SPP_CHUNKS_DEFAULT 32
+static inline int rt_resolve_spp_chunks(int spp_chunks, int spp)
+{
+    int p = spp_chunks == RT_SPP_CHUNKS_AUTO ? RT_SPP_CHUNKS_DEFAULT : spp_chunks;
+    if (p <= 1 || spp <= 1) return 1;
+    return p < spp ? p : spp;
+}
+
 /* Fills defaults: RT_RNG_PHILOX, seed 1010 (main_cuda.cu's curand seed),
- * compat_int_truncation 1, spp_chunks 1, RT_ACCEL_AUTO, everything else zero. */
+ * compat_int_truncation 1, spp_chunks RT_SPP_CHUNKS_AUTO, RT_ACCEL_AUTO,
+ * everything else zero. */
 void rt_params_init(rt_params* p);
 
 /* ---- lifecycle ---------------------------------------------------------- */
@@ -150,9 +169,22 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params,
 
 /* pthread start routine with fill_canva's exact contract (main.c:245-284):
  * arg is a struct ThreadData / rt_thread_data.  Renders start_row..end_row
- * on the GPU with the Philox stream (seed 1010).  Returns NULL on success,
- * (void*)1 on failure (see rt_last_error on that thread). */
+ * on the GPU with the Philox stream (seed 1010) and the spp_chunks grouping
+ * set by rt_set_fill_spp_chunks (default RT_SPP_CHUNKS_AUTO).  Returns NULL
+ * on success, (void*)1 on failure (see rt_last_error on that thread). */
 void* rt_fill_canva(void* thread_data);
+
+/* The spp_chunks rt_fill_canva renders with (ThreadData has no such field):
+ * RT_SPP_CHUNKS_AUTO (default, the benchmarked task-queue kernel) or an
+ * explicit P (1 = fill_canva's strict running sum, main.c:264-273).
+ * Process-wide; returns the previous setting. */
+int rt_set_fill_spp_chunks(int spp_chunks);
+
+/* rt_render_rows / rt_fill_canva keep the uploaded scene (and its BVH) of
+ * the last few distinct scenes per device, keyed by the exact bytes of the
+ * caller's arrays, so the NUM_THREADS calls of one frame upload it once.
+ * Drops them (rt_shutdown does too); returns how many were cached. */
+int rt_scene_cache_clear(void);
 
 /* ---- device-resident interface ------------------------------------------ */
 typedef struct rt_device_scene rt_device_scene;   /* opaque */

@@ -724,7 +724,7 @@ static void* band_worker(void* arg)
     init_ctx(&c, b);
     /* rt.h spp_chunks: P > 1 sums samples in P fixed slices, then the slice
      * sums in slice order; P = 1 is fill_canva's running sum (main.c:264-273) */
-    const int P = p->spp_chunks > 1 ? (p->spp_chunks < S ? p->spp_chunks : S) : 1;
+    const int P = rt_resolve_spp_chunks(p->spp_chunks, S);
     for (int j = b->start_row; j >= b->end_row; --j) {
         for (int i = 0; i < W; i++) {
             int pixel_index = j * W + i;

@@ -19,6 +19,7 @@ INC = os.path.join(ROOT, "include", "rt")
 def declared(header):
     src = open(os.path.join(INC, header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"static inline[^{;]*\{.*?\n\}", "", src, flags=re.S)   # header-only helpers
     return sorted(set(re.findall(r"\b(rt_[a-z_0-9]+)\s*\(", src)) - {"rt_version_t"})
 
 
@@ -45,7 +46,7 @@ def test_library_loads_and_reports_version():
     assert b"gfx950" in L.rt_version()
     p = T.Params()
     L.rt_params_init(C.byref(p))
-    assert p.rng == T.RT_RNG_PHILOX and p.seed == 1010 and p.compat_int_truncation == 1 and p.spp_chunks == 1
+    assert p.rng == T.RT_RNG_PHILOX and p.seed == 1010 and p.compat_int_truncation == 1 and p.spp_chunks == T.RT_SPP_CHUNKS_AUTO
 
 
 LAYOUT_C = r"""

@@ -51,8 +51,8 @@ def assert_same(gpu, ref, what):
                              (what, len(diff), j, i, c, gpu[j, i, c], ref[j, i, c]))
 
 
-def check_parity(bundle, p):
-    ref = helpers.oracle_render(bundle, p)
+def check_parity(bundle, p, nthreads=1):
+    ref = helpers.oracle_render(bundle, p, nthreads=nthreads)
     canva, alb, nrm, rad = gpu_render(bundle, p)
     fin = ~np.isnan(ref["radiance"])               # NaN radiance: the reference's own (e.g. AO 0)
     assert (np.isnan(rad) == ~fin).all()

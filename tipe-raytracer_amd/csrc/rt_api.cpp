@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -257,7 +258,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.useAO = p->useAO ? 1 : 0;
     kp.key0 = (uint32_t)p->seed;
     kp.key1 = (uint32_t)(p->seed >> 32);
-    kp.chunks = p->spp_chunks > 1 ? std::min(p->spp_chunks, p->nbRayonParPixel) : 1;
+    kp.chunks = rt_resolve_spp_chunks(p->spp_chunks, p->nbRayonParPixel);
     kp.row_base = t->row_base;
     kp.tile_rows = t->tile_rows;
     kp.tile_first = t->tile_first;
@@ -348,6 +349,134 @@ int launch_on_stream(KParams& kp, const double* uni, hipStream_t st, bool count)
     return RT_OK;
 }
 
+// ---- host-buffer drop-in plumbing (rt_render_rows / rt_fill_canva) --------
+// main.c runs fill_canva on NUM_THREADS pthreads (main.c:404-453); each of
+// them becomes one rt_render_rows call.  So that those calls neither re-upload
+// the scene (and rebuild its BVH) nor serialise on hipFree/hipStreamDestroy:
+//  * uploaded scenes are cached per device, keyed by the exact bytes of the
+//    caller's arrays (a changed array is a different scene, never stale);
+//  * streams come from a per-device pool, each with a pinned staging buffer
+//    for its D2H copy, reused across calls;
+//  * frame planes are stream-ordered allocations (hipMallocAsync) from the
+//    device pool whose release threshold launch_on_stream raises.
+std::atomic<int> g_fill_chunks{RT_SPP_CHUNKS_AUTO};
+
+struct PooledStream {
+    int device = 0;
+    hipStream_t st = nullptr;
+    void* host = nullptr;            // pinned staging for the D2H copy
+    size_t host_bytes = 0;
+    hipError_t reserve_host(size_t n)
+    {
+        if (n <= host_bytes) return hipSuccess;
+        if (host) (void)hipHostFree(host);
+        host = nullptr;
+        host_bytes = 0;
+        const hipError_t e = hipHostMalloc(&host, n, hipHostMallocDefault);
+        if (e == hipSuccess) host_bytes = n;
+        return e;
+    }
+};
+
+std::mutex g_pool_mu;
+std::vector<PooledStream*> g_pool_free;    // idle streams (any device); never destroyed
+
+int stream_pool_get(int device, PooledStream** out)
+{
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pool_free.size(); ++i)
+            if (g_pool_free[i]->device == device) {
+                *out = g_pool_free[i];
+                g_pool_free.erase(g_pool_free.begin() + (long)i);
+                return RT_OK;
+            }
+    }
+    DeviceGuard g(device);
+    PooledStream* ps = new PooledStream();
+    ps->device = device;
+    const hipError_t e = hipStreamCreateWithFlags(&ps->st, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ps;
+        return fail(RT_EDEVICE, "device %d stream: %s", device, hipGetErrorString(e));
+    }
+    *out = ps;
+    return RT_OK;
+}
+
+void stream_pool_put(PooledStream* ps)
+{
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool_free.push_back(ps);
+}
+
+// Exact bytes of everything rt_scene_upload reads.
+std::vector<unsigned char> scene_key(const rt_scene* sc)
+{
+    std::vector<unsigned char> k;
+    auto put = [&k](const void* p, size_t n) {
+        const unsigned char* b = (const unsigned char*)p;
+        k.insert(k.end(), b, b + n);
+    };
+    const int hdr[7] = {sc->nbSpheres, sc->nbTriangles, sc->tex_width, sc->tex_height, sc->nbMaterials,
+                        sc->sky_mat_list ? sc->sky_width : -1, sc->sky_mat_list ? sc->sky_height : -1};
+    put(hdr, sizeof hdr);
+    if (sc->nbSpheres > 0) put(sc->sphere_list, sizeof(rt_sphere) * (size_t)sc->nbSpheres);
+    if (sc->nbTriangles > 0) {
+        put(sc->triangle_list, sizeof(rt_triangle) * (size_t)sc->nbTriangles);
+        put(sc->quelMatPourTri, sizeof(int) * (size_t)sc->nbTriangles);
+        put(sc->mat_list, sizeof(rt_material) * (size_t)sc->nbMaterials * sc->tex_width * sc->tex_height);
+    }
+    if (sc->sky_mat_list) put(sc->sky_mat_list, sizeof(rt_material) * (size_t)sc->sky_width * sc->sky_height);
+    return k;
+}
+
+struct CachedScene {
+    int device;
+    std::vector<unsigned char> key;
+    std::shared_ptr<rt_device_scene> ds;
+    unsigned long long used;
+};
+std::mutex g_cache_mu;
+std::vector<CachedScene> g_cache;          // at most kCacheEntries, least recently used evicted
+unsigned long long g_cache_clock = 0;
+constexpr size_t kCacheEntries = 4;
+
+// The device copy of *sc on `device`, uploaded on first use.  Held under the
+// cache lock: concurrent callers of one new scene wait for its single upload.
+int scene_cache_get(int device, const rt_scene* sc, std::shared_ptr<rt_device_scene>& out)
+{
+    std::vector<unsigned char> key = scene_key(sc);
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    for (CachedScene& c : g_cache)
+        if (c.device == device && c.key == key) {
+            c.used = ++g_cache_clock;
+            out = c.ds;
+            return RT_OK;
+        }
+    rt_device_scene* ds = nullptr;
+    const int rc = rt_scene_upload(device, sc, &ds);
+    if (rc) return rc;
+    if (g_cache.size() >= kCacheEntries) {
+        size_t lru = 0;
+        for (size_t i = 1; i < g_cache.size(); ++i)
+            if (g_cache[i].used < g_cache[lru].used) lru = i;
+        g_cache.erase(g_cache.begin() + (long)lru);    // in-flight users keep their reference
+    }
+    g_cache.push_back(CachedScene{device, std::move(key), std::shared_ptr<rt_device_scene>(ds, free_scene),
+                                  ++g_cache_clock});
+    out = g_cache.back().ds;
+    return RT_OK;
+}
+
+int scene_cache_clear()
+{
+    std::lock_guard<std::mutex> lk(g_cache_mu);
+    const int n = (int)g_cache.size();
+    g_cache.clear();
+    return n;
+}
+
 }  // namespace
 
 extern "C" {
@@ -359,7 +488,7 @@ void rt_params_init(rt_params* p)
     p->rng = RT_RNG_PHILOX;
     p->seed = 1010ull;
     p->compat_int_truncation = 1;
-    p->spp_chunks = 1;
+    p->spp_chunks = RT_SPP_CHUNKS_AUTO;
 }
 
 int rt_init(int ndev, const int* devices)
@@ -383,9 +512,12 @@ int rt_init(int ndev, const int* devices)
 
 void rt_shutdown(void)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
-    g_devices.clear();
-    g_inited = false;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_devices.clear();
+        g_inited = false;
+    }
+    scene_cache_clear();
 }
 
 const char* rt_last_error(void) { return g_err.c_str(); }
@@ -699,78 +831,107 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, i
     // busiest device renders at most one tile more than the average).
     const int k = ndev == 1 ? nrows : 2;
     const int ntiles = (nrows + k - 1) / k;
+    rt_color* outs[3] = {canva, albedo, normal};
+    const int nplanes = 3;
 
     struct Slot {
-        rt_device_scene* sc = nullptr;
-        hipStream_t st = nullptr;
-        double* buf = nullptr;      // canva | albedo | normal planes
+        std::shared_ptr<rt_device_scene> sc;
+        PooledStream* ps = nullptr;
+        double* buf = nullptr;      // device planes canva | albedo | normal (only the requested ones)
         int n_tiles = 0;
-        size_t plane = 0;
+        size_t plane = 0;           // doubles per plane
     };
     std::vector<Slot> slots((size_t)ndev);
     auto cleanup = [&]() {
         for (auto& s : slots) {
-            if (s.sc) {
-                DeviceGuard g(s.sc->device);
-                if (s.st) (void)hipStreamSynchronize(s.st);
-                (void)hipFree(s.buf);
-                if (s.st) (void)hipStreamDestroy(s.st);
-            }
-            rt_scene_release(s.sc);
+            if (!s.ps) continue;
+            DeviceGuard g(s.ps->device);
+            if (s.buf) (void)hipFreeAsync(s.buf, s.ps->st);
+            (void)hipStreamSynchronize(s.ps->st);
+            stream_pool_put(s.ps);
+            s.ps = nullptr;
         }
     };
+    // 1. every device: cached scene, pooled stream, stream-ordered planes, launch
     for (int q = 0; q < ndev; ++q) {
         Slot& s = slots[(size_t)q];
         s.n_tiles = ntiles > q ? (ntiles - q + ndev - 1) / ndev : 0;
         if (s.n_tiles == 0) continue;
-        if ((rc = rt_scene_upload(devs[(size_t)q], scene, &s.sc))) {
+        if ((rc = scene_cache_get(devs[(size_t)q], scene, s.sc))) {
+            cleanup();
+            return rc;
+        }
+        if ((rc = stream_pool_get(devs[(size_t)q], &s.ps))) {
             cleanup();
             return rc;
         }
         DeviceGuard g(devs[(size_t)q]);
         s.plane = (size_t)s.n_tiles * k * W * 3;
-        hipError_t e = hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipMalloc((void**)&s.buf, s.plane * 3 * sizeof(double));
+        size_t nbuf = 0;
+        for (int pl = 0; pl < nplanes; ++pl) nbuf += outs[pl] ? s.plane : 0;
+        hipError_t e = hipMallocAsync((void**)&s.buf, nbuf * sizeof(double), s.ps->st);
         if (e != hipSuccess) {
             cleanup();
-            return fail(RT_EDEVICE, "device %d setup: %s", devs[(size_t)q], hipGetErrorString(e));
+            return fail(RT_EDEVICE, "device %d frame: %s", devs[(size_t)q], hipGetErrorString(e));
         }
         rt_tiling t{row_lo, k, q, ndev, s.n_tiles};
         KParams kp;
         double uni[U_COUNT];
-        make_kparams(s.sc, params, &t, kp, uni);
+        make_kparams(s.sc.get(), params, &t, kp, uni);
         kp.row_end = row_hi + 1;
-        kp.canva = s.buf;
-        kp.albedo = albedo ? s.buf + s.plane : nullptr;
-        kp.normal = normal ? s.buf + 2 * s.plane : nullptr;
-        if ((rc = launch_on_stream(kp, uni, s.st, false))) {
+        double* nxt = s.buf;
+        double** dst[3] = {&kp.canva, &kp.albedo, &kp.normal};
+        for (int pl = 0; pl < nplanes; ++pl) {
+            *dst[pl] = outs[pl] ? nxt : nullptr;
+            if (outs[pl]) nxt += s.plane;
+        }
+        if ((rc = launch_on_stream(kp, uni, s.ps->st, false))) {
             cleanup();
             return rc;
         }
     }
-    std::vector<double> host;
+    // 2. every device: D2H of the requested planes into its stream's pinned
+    //    staging buffer, all enqueued before any wait (the copies overlap)
     for (int q = 0; q < ndev; ++q) {
         Slot& s = slots[(size_t)q];
         if (s.n_tiles == 0) continue;
         DeviceGuard g(devs[(size_t)q]);
-        host.resize(s.plane * 3);
-        hipError_t e = hipMemcpyAsync(host.data(), s.buf, s.plane * 3 * sizeof(double), hipMemcpyDeviceToHost, s.st);
-        if (e == hipSuccess) e = hipStreamSynchronize(s.st);
+        size_t nbuf = 0;
+        for (int pl = 0; pl < nplanes; ++pl) nbuf += outs[pl] ? s.plane : 0;
+        hipError_t e = s.ps->reserve_host(nbuf * sizeof(double));
+        if (e == hipSuccess) e = hipMemcpyAsync(s.ps->host, s.buf, nbuf * sizeof(double), hipMemcpyDeviceToHost, s.ps->st);
+        if (e != hipSuccess) {
+            cleanup();
+            return fail(RT_EDEVICE, "device %d copy: %s", devs[(size_t)q], hipGetErrorString(e));
+        }
+    }
+    // 3. wait for each device in turn and scatter its rows into the caller's arrays
+    for (int q = 0; q < ndev; ++q) {
+        Slot& s = slots[(size_t)q];
+        if (s.n_tiles == 0) continue;
+        DeviceGuard g(devs[(size_t)q]);
+        const hipError_t e = hipStreamSynchronize(s.ps->st);
         if (e != hipSuccess) {
             cleanup();
             return fail(RT_EDEVICE, "device %d render/copy: %s", devs[(size_t)q], hipGetErrorString(e));
         }
-        rt_color* outs[3] = {canva, albedo, normal};
-        for (int lt = 0; lt < s.n_tiles; ++lt) {
-            const int t = q + lt * ndev;
-            for (int y = 0; y < k; ++y) {
-                const int gr = row_lo + t * k + y;
-                if (gr > row_hi) break;
-                const size_t src = ((size_t)lt * k + y) * W * 3;
-                for (int p = 0; p < 3; ++p)
-                    if (outs[p])
-                        std::memcpy(outs[p] + (size_t)gr * W, host.data() + p * s.plane + src, sizeof(double) * 3 * W);
+        const double* src0 = (const double*)s.ps->host;
+        for (int pl = 0; pl < nplanes; ++pl) {
+            if (!outs[pl]) continue;
+            if (ndev == 1) {       // one band: rows row_lo..row_hi are contiguous in both
+                std::memcpy(outs[pl] + (size_t)row_lo * W, src0, sizeof(double) * 3 * (size_t)W * nrows);
+            } else {
+                for (int lt = 0; lt < s.n_tiles; ++lt) {
+                    const int t = q + lt * ndev;
+                    for (int y = 0; y < k; ++y) {
+                        const int gr = row_lo + t * k + y;
+                        if (gr > row_hi) break;
+                        std::memcpy(outs[pl] + (size_t)gr * W, src0 + ((size_t)lt * k + y) * W * 3,
+                                    sizeof(double) * 3 * W);
+                    }
+                }
             }
+            src0 += s.plane;
         }
     }
     cleanup();
@@ -783,6 +944,12 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, i
 
 void rt_set_denoise_hook(rt_denoise_fn fn) { g_denoise.store(fn); }
 int rt_set_zero_throughput_exit(int enable) { return g_zero_exit.exchange(enable ? 1 : 0); }
+int rt_set_fill_spp_chunks(int spp_chunks)
+{
+    if (spp_chunks < RT_SPP_CHUNKS_AUTO) spp_chunks = 1;
+    return g_fill_chunks.exchange(spp_chunks);
+}
+int rt_scene_cache_clear(void) { return scene_cache_clear(); }
 rt_denoise_fn rt_get_denoise_hook(void) { return g_denoise.load(); }
 
 int rt_denoise_pack(int W, int H, const rt_color* canva, const rt_color* albedo, const rt_color* normal,
@@ -858,6 +1025,7 @@ void* rt_fill_canva(void* arg)
     p.AO_intensity = d->AO_intensity;
     p.useAO = d->useAO ? 1 : 0;
     p.compat_int_truncation = 0;
+    p.spp_chunks = g_fill_chunks.load();
     const int rc = rt_render_rows(&sc, &p, d->start_row, d->end_row, d->canva, d->albedo_tab, d->normal_tab);
     return rc == RT_OK ? nullptr : (void*)1;
 }

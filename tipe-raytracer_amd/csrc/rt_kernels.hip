@@ -2098,10 +2098,12 @@ static unsigned queue_grid(bool sky, bool bvh)
         else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<false, false>, 256, 0);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         c = std::max(1, nb) * std::max(1, ncu);
-        if (const char* e = std::getenv("RT_QUEUE_BLOCKS")) c = std::max(1, std::atoi(e));   // experiments
         if (std::getenv("RT_QUEUE_VERBOSE")) std::fprintf(stderr, "render_kernel_q: %d blocks/CU x %d CUs -> %d\n", nb, ncu, c);
         slot.store(c, std::memory_order_relaxed);
     }
+    // RT_QUEUE_BLOCKS (tests, experiments) is read on every launch, so a test
+    // can shrink the grid to a few blocks and give every lane hundreds of tasks.
+    if (const char* e = std::getenv("RT_QUEUE_BLOCKS")) c = std::max(1, std::atoi(e));
     return (unsigned)c;
 }
 #endif

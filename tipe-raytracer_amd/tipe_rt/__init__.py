@@ -11,7 +11,8 @@ import numpy as np
 
 from .types import (Vec3, Ray, Material, Sphere, UV, Triangle, Camera, ThreadData, Scene,  # noqa: F401
                     Params, Tiling, Frame, RT_OK, RT_EINVAL, RT_EDEVICE, RT_ENOMEM, RT_EUNSUPPORTED,
-                    RT_RNG_PHILOX, RT_RNG_GLIBC, RT_NCOUNTERS, COUNTER_NAMES)
+                    RT_RNG_PHILOX, RT_RNG_GLIBC, RT_NCOUNTERS, COUNTER_NAMES, RT_SPP_CHUNKS_AUTO,
+                    RT_SPP_CHUNKS_DEFAULT)
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("RT_HIP_LIB") or os.path.join(PKG_DIR, "librt_hip.so")   # override: A/B builds
@@ -66,6 +67,9 @@ def lib():
         L.rt_get_denoise_hook.restype = C.c_void_p
         L.rt_set_zero_throughput_exit.argtypes = [C.c_int]
         L.rt_set_zero_throughput_exit.restype = C.c_int
+        L.rt_set_fill_spp_chunks.argtypes = [C.c_int]
+        L.rt_set_fill_spp_chunks.restype = C.c_int
+        L.rt_scene_cache_clear.restype = C.c_int
         L.rt_denoise_pack.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6
         L.rt_denoise_unpack.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         L.rt_denoise_pack_async.argtypes = [C.c_int, C.c_int, P(Frame)] + [C.c_void_p] * 4
@@ -78,7 +82,8 @@ EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error",
                     "rt_scene_release", "rt_render_async", "rt_assemble_async", "rt_count_async",
                     "rt_selftest_math", "rt_accumulate_async", "rt_resolve_async", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
                     "rt_denoise_unpack", "rt_denoise_pack_async", "rt_verify_sampler_phi",
-                    "rt_verify_sphere_pass", "rt_set_zero_throughput_exit"]
+                    "rt_verify_sphere_pass", "rt_set_zero_throughput_exit", "rt_set_fill_spp_chunks",
+                    "rt_scene_cache_clear"]
 
 # rt_denoise_fn (rt.h): denoiser()'s signature, denoiser.h:31
 DENOISE_FN = C.CFUNCTYPE(None, C.c_int, C.c_int, C.c_void_p, Camera, C.c_void_p, C.c_void_p)

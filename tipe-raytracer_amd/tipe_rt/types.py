@@ -4,6 +4,13 @@ import ctypes as C
 
 RT_OK, RT_EINVAL, RT_EDEVICE, RT_ENOMEM, RT_EUNSUPPORTED = 0, -1, -2, -3, -4
 RT_RNG_PHILOX, RT_RNG_GLIBC = 0, 1
+RT_SPP_CHUNKS_AUTO, RT_SPP_CHUNKS_DEFAULT = -1, 32
+
+
+def rt_resolve_spp_chunks(spp_chunks, spp):
+    """rt.h rt_resolve_spp_chunks: the slice count a launch uses."""
+    p = RT_SPP_CHUNKS_DEFAULT if spp_chunks == RT_SPP_CHUNKS_AUTO else spp_chunks
+    return 1 if (p <= 1 or spp <= 1) else min(p, spp)
 
 (RT_CNT_SAMPLES, RT_CNT_CASTS, RT_CNT_SPHERE_TESTS, RT_CNT_SPHERE_DISC,
  RT_CNT_TRI_TESTS, RT_CNT_SHADE, RT_CNT_TEX_HITS, RT_CNT_REFRACT,
