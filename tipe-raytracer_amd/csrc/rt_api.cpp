@@ -255,6 +255,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     uni[U_AO] = AO;
     uni[U_WM1] = (double)(p->largeur_image - 1);    // main.c:265 (largeur_image-1)
     uni[U_HM1] = (double)(p->hauteur_image - 1);
+    uni[U_RC_WM1] = uni[U_RC_HM1] = 0.0;            // refined on the device (set_uniforms_kernel)
     kp.useAO = p->useAO ? 1 : 0;
     kp.key0 = (uint32_t)p->seed;
     kp.key1 = (uint32_t)(p->seed >> 32);
@@ -271,11 +272,6 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     double cam = 0.0;
     for (int i = 0; i < 3; ++i) cam = std::max(cam, std::fabs(p->cam.origin.e[i]));
     cam += 0.5 * (std::fabs(ox) + std::fabs(oy));
-    // camera_ray's origin co + (jx*ox, jy*oy, 0) is co itself when there is no
-    // aperture and no component of co is -0 (-0 + +0 would be +0)
-    kp.pf_two = ox == 0.0 && oy == 0.0;
-    for (int i = 0; i < 3; ++i)
-        if (p->cam.origin.e[i] == 0.0 && std::signbit(p->cam.origin.e[i])) kp.pf_two = 0;
     // Zero-throughput exit (rt_kernels.hip LanePath::zero_rc): exact when the
     // shading values are bounded and, with AO, the AO factor stays finite.
     kp.zero_exit = g_zero_exit.load() && p->semantics != RT_SEM_CUDA && sc->mats_bounded &&

@@ -58,6 +58,7 @@ static_assert(sizeof(TriTex) == 104, "TriTex");
 enum : int {
     U_CAM_O = 0, U_CAM_H = 3, U_CAM_V = 6, U_CAM_C = 9,
     U_FOCUS = 12, U_OX, U_OY, U_AO, U_WM1, U_HM1,
+    U_RC_WM1, U_RC_HM1,      // rcp_refined(W-1), rcp_refined(H-1) (device-computed), or 0: plain division
     U_COUNT
 };
 
@@ -102,8 +103,10 @@ struct KParams {
     double* partial;         // chunks > 1: [chunks][band_rows*W][9]
     double* sums;            // accumulate mode (rt_accumulate_async): [local_rows*W][9] running sums, or null
     long long s_base;        // global index of this launch's first sample (Philox counter word 3)
-    int pf_two;              // queue kernel may keep two camera directions ahead (rays start exactly at the camera origin)
     unsigned* task_ctr;      // render_kernel_q's task counter (zeroed per band launch), or null
+    unsigned npx_here;       // render_kernel_q: pixels of this band that exist (tasks = npx_here * chunks)
+    unsigned qm_npx, qm_w, qm_tile, qm_chunks;   // floor((2^32-1)/d) for d = npx_here, W, tile_rows,
+                                                 // chunks (udiv_q); qm_chunks 0: 64-bit chunk starts
     unsigned long long* trace;   // render_kernel_q diagnostics (RT_QUEUE_TRACE), normally null
     unsigned long long* counters;
 };

@@ -89,18 +89,13 @@ static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) m
 #ifndef RT_WAVES_PER_SIMD_Q         // queue kernel occupancy bound
 #define RT_WAVES_PER_SIMD_Q RT_WAVES_PER_SIMD
 #endif
-#ifndef RT_QUEUE_WAIT               // ... or once this many eighths of the lanes wait with no ray (9: never)
-#define RT_QUEUE_WAIT 9
-#endif
-#ifndef RT_PF_DEPTH                 // queue kernel: camera rays ahead per lane (2 needs no aperture)
-#define RT_PF_DEPTH 1               // (2 measured -2 % at fill 4, equal at fill 3: events are not the limit)
-#endif
-#ifndef RT_QUEUE_BVH                // queue kernel also for BVH scenes (each lane walks its own tree)
-#define RT_QUEUE_BVH 0
-#endif
 #ifndef RT_PREFETCH                 // queue kernel: camera rays computed one path ahead (LDS)
 #define RT_PREFETCH 1
 #endif
+#ifndef RT_QSTATS                   // diagnostic build: round census of render_kernel_q in the trace
+#define RT_QSTATS 0
+#endif
+#define RT_TRACE_WORDS (RT_QSTATS ? 18 : 4)
 #ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
 #define RT_WAVES_PER_SIMD_BVH 3
 #endif
@@ -1066,8 +1061,13 @@ __device__ __forceinline__ void camera_ray(const KParams& kp, int x, int g, ST& 
     const int b = opq0();
     const cdptr U = (cdptr)kp.uni;
     // main.c:265-266; main_cuda.cu:152-153 adds 0.5 first
-    const double u = (CU ? (double)x + 0.5 + ju : (double)x + ju) / U[b + U_WM1];
-    const double v = (CU ? (double)g + 0.5 + jv : (double)g + jv) / U[b + U_HM1];
+    // (x + ju) / (W - 1): the numerators are 0 or of magnitude >= 2^-31 and
+    // the divisors in [1, 2^31], inside div_core's exact range
+    const double nu = CU ? (double)x + 0.5 + ju : (double)x + ju;
+    const double nv = CU ? (double)g + 0.5 + jv : (double)g + jv;
+    const double rcw = U[b + U_RC_WM1], rch = U[b + U_RC_HM1];
+    const double u = rcw != 0.0 ? div_core(nu, U[b + U_WM1], rcw) : nu / U[b + U_WM1];
+    const double v = rch != 0.0 ? div_core(nv, U[b + U_HM1], rch) : nv / U[b + U_HM1];
     const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
     // get_ray, camera.h:42-55
     const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
@@ -1095,7 +1095,12 @@ __device__ __forceinline__ void camera_ray(const KParams& kp, int x, int g, ST& 
 // lane slots 258 -> 97 per sample (RT_BVH_SM 4, RT_BVH_SM_FILL 6).
 enum : int { SM_RESOLVE = 0, SM_CAM = 1, SM_CAST = 2, SM_TRAV = 3, SM_DONE = 4 };
 
-template <bool COUNT, bool SKY>
+// AOM: AO compiled out (0), always on (1), or read from kp.useAO (2); the
+// queue kernel is instantiated per AO setting so a sphere scene without AO
+// carries neither the AO cast's state nor its code.
+enum : int { AO_OFF = 0, AO_ON = 1, AO_RUNTIME = 2 };
+
+template <bool COUNT, bool SKY, int AOM = AO_RUNTIME>
 struct LanePath {
     Stream st;
     V3 o, d, cd;                                 // ray, next bounce direction, current cast's direction
@@ -1103,6 +1108,9 @@ struct LanePath {
     double top_n2, best;
     int i, kind, win, win_orig, node, sp, s, state;
     bool chain, ao_cast;
+#if RT_QSTATS
+    bool dbg_lit = false, dbg_phi_fb = false;    // diagnostic build: this round's lit branch / phi fallback
+#endif
 
     // Zero-throughput exit (kp.zero_exit, set by the host only when it is
     // exact): once rayColor is (0, 0, 0) every later bounce adds em * 0 = +-0
@@ -1141,7 +1149,8 @@ struct LanePath {
         bool add_inc = true;                 // false: direct view of a light (tracer returns early)
         st.k0 = kp.key0;                     // the key from the kernel argument (uniform), not
         st.k1 = kp.key1;                     // a loop-carried copy
-        if (ao_cast) {
+        const bool use_ao = AOM == AO_RUNTIME ? kp.useAO != 0 : AOM == AO_ON;
+        if (AOM != AO_OFF && ao_cast) {
             // ambient_occlusion's tail, main.c:104-115
             const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
             double occ = 0.0;
@@ -1187,6 +1196,9 @@ struct LanePath {
                     acc_add(acc, ACC_ALB, col);
                     acc_add(acc, ACC_NRM, hn);
                     lit = true;
+#if RT_QSTATS
+                    dbg_lit = true;
+#endif
                 } else if (!(mat.alpha < 0.0001) || i == kp.B - 1) {
                     acc_add(acc, ACC_ALB, mat.diff);
                     acc_add(acc, ACC_NRM, hn);
@@ -1231,7 +1243,7 @@ struct LanePath {
                 }
                 if (shade) {
                     V3 r = rc;
-                    if (kp.useAO) {
+                    if (use_ao) {
                         const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
                         const V3 em = muls(mat.emis, mat.es * 1.5 * AO);
                         inc = inc + mulv(em, r);
@@ -1253,7 +1265,7 @@ struct LanePath {
                 }
             }
         }
-        if (ao_cast) {
+        if (AOM != AO_OFF && ao_cast) {
             state = SM_CAST;
         } else {
             if (more) {
@@ -1756,8 +1768,30 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
 // atomic per lane grab was 1.8x slower (same-address atomics).  The grid is
 // the resident capacity; every lane leaves once the counter passes the
 // task count.
-template <bool SKY, bool BVH>
-__global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
+// n / d and n % d for 32-bit n by a launch-constant d with m = kp's
+// floor((2^32 - 1) / d) (host, qdiv_magic): the high product is q or q - 1,
+// one remainder check fixes it (5 integer ops instead of a division).
+__device__ __forceinline__ unsigned udiv_q(unsigned n, unsigned d, unsigned m, unsigned& r)
+{
+    unsigned q = __umulhi(n, m);
+    const unsigned rr = n - q * d;
+    const bool up = rr >= d;
+    r = up ? rr - d : rr;
+    return up ? q + 1u : q;
+}
+
+// First sample of chunk c: c*S/P (exact; 32-bit when S*P < 2^32).
+__device__ __forceinline__ int chunk_start(const KParams& kp, unsigned c)
+{
+    if (kp.qm_chunks != 0u) {
+        unsigned r;
+        return (int)udiv_q(c * (unsigned)kp.S, (unsigned)kp.chunks, kp.qm_chunks, r);
+    }
+    return (int)(((long long)c * kp.S) / kp.chunks);
+}
+
+template <bool SKY, int AOM>
+__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
 {
     __shared__ double acc_lds[ACC_INC * 256];
     __shared__ double pf_lds[(RT_PREFETCH ? 6 : 1) * 256];   // a camera ray computed ahead (o, d)
@@ -1768,43 +1802,43 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
     Cnt cnt;
     const unsigned npx = (unsigned)kp.band_rows * (unsigned)kp.W;     // partials' chunk stride
     // tasks cover the rows of this band that exist (the last band is shorter)
-    const int rows_here = min(kp.band_rows, kp.local_rows - kp.band_y0);
-    const unsigned npx_here = (unsigned)max(rows_here, 0) * (unsigned)kp.W;
+    const unsigned npx_here = kp.npx_here;
     const unsigned ntask = npx_here * (unsigned)kp.chunks;
     unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
-    LanePath<false, SKY> L;
+    LanePath<false, SKY, AOM> L;
     L.init(0, 1);                    // SM_CAM with s = 0 >= s1 = 0: takes a task first
     int x = 0, g = 0, s1 = 0;
     unsigned chunk = 0, p = 0, pixel = 0;
     bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
     const long long t_start = kp.trace ? wall_clock64() : 0;
     unsigned rounds = 0, ntasks = 0;
-    // Camera rays computed ahead live in pf: with kp.pf_two (no aperture, so
-    // every ray starts exactly at the camera origin) up to two directions, of
-    // samples s+1 and s+2 in slots (s & 1); otherwise one ray (o, d).
-    // pf_hi: the last sample of the task whose ray is computed (in flight or
-    // in pf).
+#if RT_QSTATS
+    // diagnostic build only: wave-level census of the rounds (lane 0 keeps it)
+    unsigned long long qs[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tq = __builtin_amdgcn_s_memtime();
+#define QT(slot)                                                   \
+    {                                                              \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        qs[slot] += t_ - tq;                                       \
+        tq = t_;                                                   \
+    }
+#else
+#define QT(slot)
+#endif
+    // A camera ray computed ahead (origin, direction) lives in pf; pf_hi is
+    // the last sample of the task whose ray is computed (in flight or in pf).
     int pf_hi = -1;
     double* pf = pf_lds + threadIdx.x;
     const bool prefetch = RT_PREFETCH && kp.B > 0;
-    const int depth = (RT_PF_DEPTH >= 2 && kp.pf_two) ? 2 : 1;
     while (L.state != SM_DONE) {
         ++rounds;
-        if (L.state == SM_CAM && L.s < s1 && pf_hi >= L.s) {    // path done, next sample's ray is ready
-            if (depth == 2) {
-                const cdptr U = (cdptr)kp.uni;
-                const int b = opq0();
-                L.begin(kp, pixel, v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]),
-                        lds_get(pf, 3 * (L.s & 1)), rng, acc, cnt);
-            } else {
-                L.begin(kp, pixel, lds_get(pf, 0), lds_get(pf, 3), rng, acc, cnt);
-            }
-        }
+        if (L.state == SM_CAM && L.s < s1 && pf_hi >= L.s)      // path done, next sample's ray is ready
+            L.begin(kp, pixel, lds_get(pf, 0), lds_get(pf, 3), rng, acc, cnt);
+        QT(12)                       // begin from a prefetched ray
         const unsigned long long live = __ballot(1), wait = __ballot(L.state == SM_CAM);
         // lanes with no ray ready for their next path
         const unsigned long long lack = __ballot(prefetch && L.state == SM_CAST && pf_hi <= L.s && L.s + 1 < s1);
-        const bool go = wait == live || (__popcll(wait) + __popcll(lack)) * 8 >= __popcll(live) * RT_QUEUE_FILL ||
-                        __popcll(wait) * 8 >= __popcll(live) * RT_QUEUE_WAIT;
+        const bool go = wait == live || (__popcll(wait) + __popcll(lack)) * 8 >= __popcll(live) * RT_QUEUE_FILL;
         const bool need = go && L.state == SM_CAM && L.s >= s1;
         const unsigned long long nm = __ballot(need);
         unsigned t = 0;
@@ -1823,6 +1857,7 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
                 qb += n;
             }
         }
+        QT(13)                       // ballots, batch grab
         if (need) {
             ++ntasks;
             if (owns) {              // task done: its sums to the chunk partials
@@ -1834,20 +1869,23 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
             if (t >= ntask) {
                 L.state = SM_DONE;
             } else {
-                chunk = t / npx_here;
-                p = t - chunk * npx_here;
-                const int ly = kp.band_y0 + (int)(p / (unsigned)kp.W);
-                x = (int)(p % (unsigned)kp.W);
+                // task t = (chunk, pixel p of the band): launch-constant divisors
+                chunk = udiv_q(t, npx_here, kp.qm_npx, p);
+                unsigned xr;
+                const unsigned row = udiv_q(p, (unsigned)kp.W, kp.qm_w, xr);
+                const int ly = kp.band_y0 + (int)row;
+                x = (int)xr;
                 bool valid = ly < kp.local_rows;
                 if (valid) {
-                    const int lt = ly / kp.tile_rows, yy = ly - lt * kp.tile_rows;
-                    g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + yy;
+                    unsigned yy;
+                    const int lt = (int)udiv_q((unsigned)ly, (unsigned)kp.tile_rows, kp.qm_tile, yy);
+                    g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + (int)yy;
                     valid = g < kp.row_end;
                 }
                 if (valid) {         // otherwise the lane takes its next task next time
                     pixel = (uint32_t)g * (uint32_t)kp.W + (uint32_t)x;
-                    L.s = (int)(((long long)chunk * kp.S) / kp.chunks);
-                    s1 = (int)(((long long)(chunk + 1) * kp.S) / kp.chunks);
+                    L.s = chunk_start(kp, chunk);
+                    s1 = chunk_start(kp, chunk + 1u);
 #pragma unroll
                     for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
                     owns = true;
@@ -1855,9 +1893,14 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
                 }
             }
         }
+        QT(8)                        // task hand-out
         if (go) {                    // one camera ray per lane: its next path's, or one ahead
             const bool now = L.state == SM_CAM && L.s < s1;
-            const bool pre = prefetch && L.state == SM_CAST && pf_hi < min(L.s + depth, s1 - 1);
+            const bool pre = prefetch && L.state == SM_CAST && pf_hi < min(L.s + 1, s1 - 1);
+#if RT_QSTATS
+            qs[2] += 1;                                         // event rounds
+            qs[3] += (unsigned long long)__popcll(__ballot(now || pre));   // lanes computing a camera ray
+#endif
             if (now && !prefetch) {
                 L.start(kp, x, g, pixel, s1, rng, acc, cnt);
             } else if (now || pre) {
@@ -1868,25 +1911,47 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
                 pf_hi = cs;
                 if (now) {
                     L.begin(kp, pixel, no, rd, rng, acc, cnt);
-                } else if (depth == 2) {
-                    lds_put(pf, 3 * (cs & 1), rd);
                 } else {
                     lds_put(pf, 0, no);
                     lds_put(pf, 3, rd);
                 }
             }
         }
+#if RT_QSTATS
+        {
+            const unsigned long long c = __ballot(L.state == SM_CAST);
+            qs[0] += 1;                                         // rounds
+            qs[1] += (unsigned long long)__popcll(c);           // lanes casting
+            qs[4] += (unsigned long long)__popcll(__ballot(L.state == SM_CAM));    // lanes waiting
+            qs[7] += c ? 1 : 0;                                 // rounds with a cast
+        }
+        QT(9)                        // camera-ray events (every QT outside divergent code)
+        if (L.state == SM_CAST) L.cast_flat(kp, cnt);
+        QT(10)                       // cast
+        L.dbg_lit = false;
+        if (L.state == SM_RESOLVE) L.resolve(kp, acc, cnt);
+        QT(11)                       // resolve
+        {
+            const unsigned long long lm = __ballot(L.dbg_lit);
+            qs[6] += lm ? 1 : 0;                                // rounds with a lit (HSL) lane
+            qs[5] += (unsigned long long)__popcll(lm);          // lit lanes
+        }
+#else
         if (L.state == SM_CAST) {
-            L.template cast_flat<BVH>(kp, cnt);
+            L.cast_flat(kp, cnt);
             L.resolve(kp, acc, cnt);
         }
+#endif
     }
     if (kp.trace) {                  // diagnostics (RT_QUEUE_TRACE): per lane start, end, rounds, tasks
-        unsigned long long* q = kp.trace + ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+        unsigned long long* q = kp.trace + ((size_t)blockIdx.x * 256 + threadIdx.x) * RT_TRACE_WORDS;
         q[0] = (unsigned long long)t_start;
         q[1] = (unsigned long long)wall_clock64();
         q[2] = rounds;
         q[3] = ntasks;
+#if RT_QSTATS
+        for (int j = 0; j < 14; ++j) q[4 + j] = qs[j];
+#endif
     }
 }
 #endif
@@ -1950,9 +2015,20 @@ __global__ __launch_bounds__(256) void assemble_kernel(const double* __restrict_
 // Per-launch uniform block: the values travel as this kernel's by-value
 // argument (captured at enqueue), so the copy is stream-ordered without a
 // pageable host staging buffer.
+// The camera's (W-1) and (H-1) reciprocals are refined here on the device
+// (rcp_refined is the device's own sequence) so camera_ray divides with
+// div_core; 0 (W or H of 1, a zero divisor) selects the plain division.
 __global__ void set_uniforms_kernel(const UniBlock u, double* __restrict__ dst)
 {
-    if (threadIdx.x < U_COUNT) dst[threadIdx.x] = u.v[threadIdx.x];
+    const int i = threadIdx.x;
+    if (i < U_COUNT) {
+        double v = u.v[i];
+        if (i == U_RC_WM1 || i == U_RC_HM1) {
+            const double d = u.v[i == U_RC_WM1 ? U_WM1 : U_HM1];
+            v = (d >= 1.0 && d <= 0x1p400) ? rcp_refined(d) : 0.0;
+        }
+        dst[i] = v;
+    }
 }
 
 int launch_set_uniforms(const UniBlock& u, double* d_uni, void* stream)
@@ -2079,23 +2155,29 @@ static void launch_variant(const KParams& kp, void* stream)
 }
 
 #if RT_QUEUE > 0
+template <bool SKY, int AOM>
+static void queue_occupancy(int& nb)
+{
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<SKY, AOM>, 256, 0);
+}
+
 // Resident blocks of the queue kernel on this device (grid of render_kernel_q).
 // Cached per device and variant; rt_fill_canva may run on several host
 // threads at once (main.c's pthreads), so the cache is atomic (every thread
 // computes the same value).
-static unsigned queue_grid(bool sky, bool bvh)
+static unsigned queue_grid(bool sky, bool ao)
 {
     static std::atomic<int> cached[4][64];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (bvh ? 2 : 0)][dev & 63];
+    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0)][dev & 63];
     int c = slot.load(std::memory_order_relaxed);
     if (c <= 0) {
         int nb = 0, ncu = 0;
-        if (bvh && sky) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<true, true>, 256, 0);
-        else if (bvh) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<false, true>, 256, 0);
-        else if (sky) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<true, false>, 256, 0);
-        else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<false, false>, 256, 0);
+        if (sky && ao) queue_occupancy<true, AO_ON>(nb);
+        else if (sky) queue_occupancy<true, AO_OFF>(nb);
+        else if (ao) queue_occupancy<false, AO_ON>(nb);
+        else queue_occupancy<false, AO_OFF>(nb);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         c = std::max(1, nb) * std::max(1, ncu);
         if (std::getenv("RT_QUEUE_VERBOSE")) std::fprintf(stderr, "render_kernel_q: %d blocks/CU x %d CUs -> %d\n", nb, ncu, c);
@@ -2106,28 +2188,38 @@ static unsigned queue_grid(bool sky, bool bvh)
     if (const char* e = std::getenv("RT_QUEUE_BLOCKS")) c = std::max(1, std::atoi(e));
     return (unsigned)c;
 }
+
+// floor((2^32 - 1) / d) for udiv_q
+static unsigned qdiv_magic(unsigned d) { return d ? (unsigned)(0xffffffffull / d) : 0u; }
 #endif
 
 int launch_render(const KParams& kp, void* stream)
 {
 #if RT_QUEUE > 0
-    if (kp.task_ctr && kp.chunks > 1 && (!kp.bvh || RT_QUEUE_BVH) && !kp.cuda && !kp.sums) {
+    if (kp.task_ctr && kp.chunks > 1 && !kp.bvh && !kp.cuda && !kp.sums) {
         const hipStream_t st = (hipStream_t)stream;
-        const bool sky = kp.sky != nullptr;
+        const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
-        const bool bvh = kp.bvh != nullptr;
-        const unsigned nb = queue_grid(sky, bvh);
+        const unsigned nb = queue_grid(sky, ao);
         unsigned long long* tr = nullptr;
         const char* tf = std::getenv("RT_QUEUE_TRACE");
-        if (tf) (void)hipMalloc((void**)&tr, (size_t)nb * 256 * 4 * sizeof(unsigned long long));
+        if (tf) (void)hipMalloc((void**)&tr, (size_t)nb * 256 * RT_TRACE_WORDS * sizeof(unsigned long long));
         KParams k2 = kp;
         k2.trace = tr;
-        if (bvh && sky) hipLaunchKernelGGL((render_kernel_q<true, true>), dim3(nb), dim3(256), 0, st, k2);
-        else if (bvh) hipLaunchKernelGGL((render_kernel_q<false, true>), dim3(nb), dim3(256), 0, st, k2);
-        else if (sky) hipLaunchKernelGGL((render_kernel_q<true, false>), dim3(nb), dim3(256), 0, st, k2);
-        else hipLaunchKernelGGL((render_kernel_q<false, false>), dim3(nb), dim3(256), 0, st, k2);
+        const int rows_here = std::max(0, std::min(kp.band_rows, kp.local_rows - kp.band_y0));
+        k2.npx_here = (unsigned)rows_here * (unsigned)kp.W;
+        k2.qm_npx = qdiv_magic(k2.npx_here);
+        k2.qm_w = qdiv_magic((unsigned)kp.W);
+        k2.qm_tile = qdiv_magic((unsigned)kp.tile_rows);
+        // chunk starts c*S/P in 32 bits when (P + 1) * S fits
+        k2.qm_chunks = (unsigned long long)(kp.chunks + 1) * (unsigned long long)kp.S < (1ull << 32)
+                           ? qdiv_magic((unsigned)kp.chunks) : 0u;
+        if (sky && ao) hipLaunchKernelGGL((render_kernel_q<true, AO_ON>), dim3(nb), dim3(256), 0, st, k2);
+        else if (sky) hipLaunchKernelGGL((render_kernel_q<true, AO_OFF>), dim3(nb), dim3(256), 0, st, k2);
+        else if (ao) hipLaunchKernelGGL((render_kernel_q<false, AO_ON>), dim3(nb), dim3(256), 0, st, k2);
+        else hipLaunchKernelGGL((render_kernel_q<false, AO_OFF>), dim3(nb), dim3(256), 0, st, k2);
         if (tr) {
-            std::vector<unsigned long long> h((size_t)nb * 256 * 4);
+            std::vector<unsigned long long> h((size_t)nb * 256 * RT_TRACE_WORDS);
             (void)hipStreamSynchronize(st);
             (void)hipMemcpy(h.data(), tr, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost);
             (void)hipFree(tr);

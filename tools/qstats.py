@@ -1,0 +1,48 @@
+"""Round census of render_kernel_q (diagnostic build -DRT_QSTATS=1).
+
+    RT_HIP_LIB=tools/variants/qstats.so python tools/qstats.py [spp] [scene]
+
+Renders one C2-shaped frame with RT_QUEUE_TRACE and reports, per wave:
+rounds, lane utilisation of the cast+resolve pass, camera-ray events and
+their lane utilisation, lanes waiting (SM_CAM) or done during casts."""
+import os
+import sys
+import json
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tipe-raytracer_amd"))
+import torch  # noqa: E402
+import tipe_rt  # noqa: E402
+from tipe_rt import scenes  # noqa: E402
+
+spp = int(sys.argv[1]) if len(sys.argv) > 1 else 250
+kind = sys.argv[2] if len(sys.argv) > 2 else "c2"
+path = os.path.join(ROOT, "gpurun_out", "qstats.bin")
+if os.path.exists(path):
+    os.remove(path)
+os.environ["RT_QUEUE_TRACE"] = path
+cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
+sph = scenes.cornell_spheres()
+sc = tipe_rt.make_scene(sph) if kind == "c2" else tipe_rt.make_scene(sph, *scenes.pyramid_mesh())
+p = tipe_rt.make_params(1200, 900, spp, 6, cam, focus=3.0, seed=1010, chunks=32)
+ds = tipe_rt.DeviceScene(sc, 0)
+out = torch.empty((3, 900, 1200, 3), dtype=torch.float64, device="cuda:0")
+tipe_rt.render_async(ds, p, tipe_rt.band_tiling(0, 899), out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(),
+                     None, torch.cuda.current_stream().cuda_stream)
+torch.cuda.synchronize()
+del os.environ["RT_QUEUE_TRACE"]
+d = np.fromfile(path, dtype=np.uint64).reshape(-1, 18)
+w = d[::64]                                  # lane 0 of each wave holds the wave census
+q = w[:, 4:12].astype(np.float64)
+t = w[:, 12:18].astype(np.float64).sum(0)
+tot = q.sum(0)
+rounds, cast_l, ev, ev_l, wait_l, done_l, task_r, cast_r = tot
+res = {"spp": spp, "scene": kind, "waves": int(len(w)), "rounds_per_wave": rounds / len(w),
+       "cast_lane_util": cast_l / (64 * cast_r), "rounds_with_cast_frac": cast_r / rounds,
+       "event_rounds_frac": ev / rounds, "event_lane_util": ev_l / (64 * ev),
+       "wait_lane_frac": wait_l / (64 * rounds), "lit_lanes_per_lit_round": done_l / max(task_r, 1),
+       "lit_rounds_frac": task_r / rounds,
+       "time_share": {k: round(v / t.sum(), 4) for k, v in zip(("task", "events", "cast", "resolve", "begin", "ballots"), t)},
+       "lane_casts_total": cast_l, "samples": 1200 * 900 * spp, "casts_per_sample": cast_l / (1200 * 900 * spp)}
+print(json.dumps(res))
