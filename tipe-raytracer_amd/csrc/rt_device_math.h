@@ -98,6 +98,15 @@ struct Philox {
     uint32_t w0, w1, w2, w3;
 };
 
+// a ^ b ^ k in one VALU op: gfx950's v_bitop3_b32 with truth table 0x96
+// (three-input xor; k a wave-uniform SGPR)
+__device__ __forceinline__ uint32_t xor3_s(uint32_t a, uint32_t b, uint32_t k)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+
 template <bool UNIFORM_KEY = true>
 __device__ __forceinline__ Philox philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                                 uint32_t k0, uint32_t k1)
@@ -105,9 +114,17 @@ __device__ __forceinline__ Philox philox4x32_10(uint32_t c0, uint32_t c1, uint32
     if (UNIFORM_KEY) asm volatile("" : "+s"(k0), "+s"(k1));   // key schedule in place (SALU), not hoisted
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        // one v_mad_u64_u32 yields both halves of each 32x32 product
+        // one v_mad_u64_u32 yields both halves of each 32x32 product; the
+        // round's two xors with the key are one v_bitop3_b32 each
         const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
-        const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n0, n2;
+        if (UNIFORM_KEY) {
+            n0 = xor3_s((uint32_t)(p1 >> 32), c1, k0);
+            n2 = xor3_s((uint32_t)(p0 >> 32), c3, k1);
+        } else {
+            n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+            n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        }
         c0 = n0; c1 = (uint32_t)p1; c2 = n2; c3 = (uint32_t)p0;
         k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
     }

@@ -1561,16 +1561,48 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
     const int lane = threadIdx.x & 63;
     LanePath<COUNT, SKY> L;
     L.init(s0, s1);
+#if RT_QSTATS
+    // diagnostic build: [0] loop rounds [1] coop phases [2] coop iterations
+    // [3] lanes with a task per coop iteration [4] parked lanes per phase
+    // [5] lanes resolving [6] lanes starting [7] lanes casting; time [8]
+    // resolve+start [9] cast+root [10] coop
+    unsigned long long qs[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tq = __builtin_amdgcn_s_memtime();
+#define QTB(slot)                                                  \
+    {                                                              \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        qs[slot] += t_ - tq;                                       \
+        tq = t_;                                                   \
+    }
+#else
+#define QTB(slot)
+#endif
     while (L.state != SM_DONE) {
+#if RT_QSTATS
+        qs[0] += 1;
+        qs[5] += (unsigned long long)__popcll(__ballot(L.state == SM_RESOLVE));
+#endif
         if (L.state == SM_RESOLVE) L.resolve(kp, acc, cnt);
+#if RT_QSTATS
+        qs[6] += (unsigned long long)__popcll(__ballot(L.state == SM_CAM));
+#endif
         if (L.state == SM_CAM) L.start(kp, x, g, pixel, s1, rng, acc, cnt);
+        QTB(8)
+#if RT_QSTATS
+        qs[7] += (unsigned long long)__popcll(__ballot(L.state == SM_CAST));
+#endif
         if (L.state == SM_CAST) {
             L.cast(kp, cnt);
             L.trav(kp, stk, 1, cnt);             // the root node; SM_TRAV: parked
         }
+        QTB(9)
         const unsigned long long parked = __ballot(L.state == SM_TRAV);
         const unsigned long long movable = __ballot(L.state == SM_RESOLVE || L.state == SM_CAM);
         if (parked == 0ull || (__popcll(parked) < RT_BVH_COOP && movable != 0ull)) continue;
+#if RT_QSTATS
+        qs[1] += 1;
+        qs[4] += (unsigned long long)__popcll(parked);
+#endif
 
         // ---- cooperative phase (wave-uniform) ----
         int qn = 0;
@@ -1588,6 +1620,9 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
         int tr = 0, tnode = 0, tsp = 0;
         V3 to = v3(0, 0, 0), td = to, tinv = to;
         for (;;) {
+#if RT_QSTATS
+            qs[2] += 1;
+#endif
             const unsigned long long idle = __ballot(!has);
             const int take = min(__popcll(idle), qn);
             bool fresh = false;
@@ -1605,6 +1640,9 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
             qn -= take;
             __builtin_amdgcn_wave_barrier();
             if (__ballot(has) == 0ull) break;
+#if RT_QSTATS
+            qs[3] += (unsigned long long)__popcll(__ballot(has));
+#endif
             // the owner's ray for new tasks, its current record for every task
             // (all live lanes run the permutes; owners are live)
             if (__ballot(fresh) != 0ull) {
@@ -1647,7 +1685,12 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
             }
         }
         if (L.state == SM_TRAV) L.state = SM_RESOLVE;
+        QTB(10)
     }
+#if RT_QSTATS
+    if (kp.trace && (threadIdx.x & 63) == 0)
+        for (int j = 0; j < 11; ++j) atomicAdd(kp.trace + j, qs[j]);
+#endif
 }
 #endif
 
@@ -1790,30 +1833,251 @@ __device__ __forceinline__ int chunk_start(const KParams& kp, unsigned c)
     return (int)(((long long)c * kp.S) / kp.chunks);
 }
 
+// One lane's path in render_kernel_q: tracer's state (main.c:118-242) for
+// the sample in flight.  Rounds run in three steps so that a lane whose path
+// ends starts its next sample's camera ray in the SAME instructions that
+// continuing lanes use for their bounce direction (one Philox block and one
+// normalize serve both):
+//   resolve_hit   everything of tracer's bounce body that does not need the
+//                 next direction: hit point, material, albedo/normal chain,
+//                 the light seen directly, alpha holes, and -- when the
+//                 surface is opaque -- the shading, the zero-throughput exit
+//                 and the bounce budget; it leaves the lane a role
+//   next_ray      BOUNCE: random_dir_no_norm and normalize(n + dir)
+//                 CAMERA: the 4 camera draws and get_ray, normalize
+//                 (both: draws from one Philox block, one normalize)
+//   finish_bounce reflect/lerp, the refraction branch (whose draw follows
+//                 the direction draws), AO set-up
+// The draws keep the reference's per-sample order (counter-based stream:
+// direction n, n+1, refraction n+2, AO next), so results are bit-identical
+// to trace(); work whose result cannot reach the output is skipped: the
+// direction after the last bounce, and the AO cast of the last bounce
+// (tracer multiplies rayColor by it and then returns incomingLight).
+enum : int { ROLE_NONE = 0, ROLE_BOUNCE = 1, ROLE_CAMERA = 2 };
+
+template <bool SKY, int AOM>
+struct QPath {
+    V3 o, d, cd, inc, rc, hn;        // cd: the cast's direction (AO casts; else d)
+    double top_n2, best, rs;
+    int i, kind, win, s, state;
+    bool chain, ao_cast, refr, hole;
+
+    __device__ __forceinline__ V3 cast_dir() const { return AOM == AO_ON ? cd : d; }
+
+    // The hit's material (tri_material / sky_material are pure functions of
+    // the hit, so a refraction lane recomputes it instead of keeping it live).
+    __device__ __forceinline__ Mat hit_material(const KParams& kp, V3 hp) const
+    {
+        if (kind == HIT_SPHERE) {
+            Mat mat = load_mat(kp.sph_mat + win);
+            if (SKY && win == kp.ns - 1) sky_material(kp, win, kp.sph[win], hp, mat);
+            return mat;
+        }
+        return tri_material(kp, win, hp, hn);
+    }
+
+    __device__ __forceinline__ bool zero_rc(const KParams& kp) const
+    {
+        return kp.zero_exit && rc.x == 0.0 && rc.y == 0.0 && rc.z == 0.0;
+    }
+
+    // After a cast (state SM_RESOLVE).  Returns the role for next_ray, or
+    // ROLE_NONE; a lane whose path is over gets state SM_CAM (sum added).
+    __device__ __forceinline__ int resolve_hit(const KParams& kp, double* acc)
+    {
+        bool ended = false, add_inc = true;
+        int role = ROLE_NONE;
+        if (AOM == AO_ON && ao_cast) {
+            // ambient_occlusion's tail, main.c:104-115
+            const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
+            double occ = 0.0;
+            if (kind != HIT_NONE) {
+                const V3 hp = o + muls(cast_dir(), best);
+                const V3 df = hp - o;
+                const double distance = sqrt(dot(df, df));
+                double att = distance / best;
+                att = pm_pow(att, AO);
+                occ = occ + att;
+            }
+            occ = (occ / 1.0) / AO;
+            rc = mulv(rc, v3(occ, occ, occ));
+            ao_cast = false;
+            ++i;                                         // the bounce after the AO cast
+            ended = zero_rc(kp) || i >= kp.B;
+            if (!ended) {
+                cd = d;
+                state = SM_CAST;
+            }
+        } else if (kind == HIT_NONE) {                   // miss: the path ends, main.c:236-238
+            if (chain) {
+                acc_add(acc, ACC_ALB, v3(0, 0, 0));
+                acc_add(acc, ACC_NRM, v3(0, 0, 0));
+            }
+            ended = true;
+        } else {
+            const V3 hp = o + muls(d, best);             // ray_at
+            if (kind == HIT_SPHERE) {
+                const SphGeo sg = kp.sph[win];
+                hn = normalize(hp - v3(sg.cx, sg.cy, sg.cz));
+            } else {
+                const TriGeo tg = kp.tri[win];
+                hn = normalize(v3(tg.nx, tg.ny, tg.nz));
+            }
+            const Mat mat = hit_material(kp, hp);
+            bool lit = false;
+            if (chain) {
+                if (mat.es > 0) {                        // direct view of a light, main.c:154-160
+                    const V3 col = hsl_roundtrip(mat.emis);
+                    acc_add(acc, ACC_RAD, col);
+                    acc_add(acc, ACC_ALB, col);
+                    acc_add(acc, ACC_NRM, hn);
+                    lit = true;
+                } else if (!(mat.alpha < 0.0001) || i == kp.B - 1) {
+                    acc_add(acc, ACC_ALB, mat.diff);
+                    acc_add(acc, ACC_NRM, hn);
+                    chain = mat.alpha < 0.0001;
+                }
+            }
+            if (lit) {
+                ended = true;
+                add_inc = false;
+            } else {
+                o = hp;
+                rs = mat.rs;
+                refr = false;
+                hole = mat.alpha < 0.0001;
+                if (hole) {                              // alpha hole: straight on, main.c:200-206;
+                    if (i + 1 >= kp.B) ended = true;     // its direction draws are made (and unused)
+                    else role = ROLE_BOUNCE;             // so the stream's block cache stays in order
+                } else {
+                    chain = false;
+                    if (mat.alpha <= 0.99) {             // refraction: decided after the direction draws
+                        refr = true;
+                        role = ROLE_BOUNCE;
+                    } else {
+                        shade(kp, mat);
+                        if (zero_rc(kp) || i + 1 >= kp.B) ended = true;   // nothing more reaches the sum
+                        else role = ROLE_BOUNCE;
+                    }
+                }
+            }
+        }
+        if (ended) {
+            if (add_inc) acc_add(acc, ACC_RAD, inc);
+            ++s;
+            state = SM_CAM;
+            role = ROLE_NONE;
+        }
+        return role;
+    }
+
+    // shading of an opaque surface (main.c:208-234 without the AO cast)
+    __device__ __forceinline__ void shade_with(const KParams& kp, V3 emis, double es, V3 diff)
+    {
+        V3 r = rc;
+        if (AOM == AO_ON) {
+            const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
+            const V3 em = muls(emis, es * 1.5 * AO);
+            inc = inc + mulv(em, r);
+        } else {
+            const V3 em = muls(emis, es);
+            inc = inc + mulv(em, r);
+        }
+        if (r.x > 0.5 || r.y > 0.5 || r.z > 0.5) r = mulv(diff, muls(r, 1.3));
+        rc = mulv(diff, r);
+    }
+    __device__ __forceinline__ void shade(const KParams& kp, const Mat& mat) { shade_with(kp, mat.emis, mat.es, mat.diff); }
+
+    // After next_ray gave a bounce lane its diffuse direction dn.
+    __device__ __forceinline__ void finish_bounce(const KParams& kp, V3 dn, Stream& st, double* acc)
+    {
+        if (hole) {                                      // the ray goes on unchanged from the hit point
+            ++i;
+            cd = d;
+            state = SM_CAST;
+            return;
+        }
+        const V3 reflected_dir = d - muls(hn, 2 * dot(d, hn));
+        const V3 dr = dn + muls(reflected_dir - dn, rs);
+        bool shaded = true;
+        if (refr) {                                      // main.c:167-193
+            const Mat mat = hit_material(kp, o);
+            V3 nn = hn;
+            double n1, n2;
+            if (dot(d, hn) > 0) {                        // leaving: pop restores the stack
+                nn = v3(-hn.x, -hn.y, -hn.z);
+                n1 = mat.ior;
+                n2 = top_n2;
+            } else {                                     // entering: push (top.n2, ior)
+                n1 = top_n2;
+                n2 = mat.ior;
+                top_n2 = mat.ior;
+            }
+            const V3 rf = refracted(d, nn, n1, n2);
+            const double rnd = 0.0 + 1.0 * unit31(st.next31());
+            if (rnd > mat.alpha) {
+                d = rf;
+                shaded = false;
+            } else {
+                d = dr;
+                shade(kp, mat);
+            }
+        } else {
+            d = dr;
+        }
+        bool ended = false;
+        if (refr && shaded) ended = zero_rc(kp);
+        if (AOM == AO_ON && shaded && !ended && i + 1 < kp.B) {
+            // ambient_occlusion's cast (main.c:96-103): from the hit along n + random
+            Cnt cnt;
+            cd = normalize(hn + random_dir<false>(st, cnt));
+            ao_cast = true;
+            state = SM_CAST;
+            return;
+        }
+        ++i;
+        ended = ended || i >= kp.B;
+        if (ended) {                                     // (refraction lanes only) the sample is over
+            acc_add(acc, ACC_RAD, inc);
+            ++s;
+            state = SM_CAM;
+        } else {
+            cd = d;
+            state = SM_CAST;
+        }
+    }
+};
+
 template <bool SKY, int AOM>
 __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
 {
     __shared__ double acc_lds[ACC_INC * 256];
-    __shared__ double pf_lds[(RT_PREFETCH ? 6 : 1) * 256];   // a camera ray computed ahead (o, d)
     __shared__ uint32_t rng_lds[4 * 256];
     double* acc = acc_lds + threadIdx.x;
     uint32_t* rng = rng_lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
-    Cnt cnt;
     const unsigned npx = (unsigned)kp.band_rows * (unsigned)kp.W;     // partials' chunk stride
-    // tasks cover the rows of this band that exist (the last band is shorter)
-    const unsigned npx_here = kp.npx_here;
+    const unsigned npx_here = kp.npx_here;            // pixels of this band that exist
     const unsigned ntask = npx_here * (unsigned)kp.chunks;
     unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
-    LanePath<false, SKY, AOM> L;
-    L.init(0, 1);                    // SM_CAM with s = 0 >= s1 = 0: takes a task first
+    QPath<SKY, AOM> L;
+    L.o = L.d = L.cd = L.inc = L.rc = L.hn = v3(0, 0, 0);
+    L.top_n2 = 1.0;
+    L.best = L.rs = 0.0;
+    L.i = 0; L.kind = HIT_NONE; L.win = -1; L.s = 0;
+    L.chain = true; L.ao_cast = false; L.refr = false; L.hole = false;
+    L.state = SM_CAM;                // s = 0 >= s1 = 0: takes a task first
     int x = 0, g = 0, s1 = 0;
     unsigned chunk = 0, p = 0, pixel = 0;
     bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
+    Stream st;                       // draw stream of the sample in flight (next31 for refraction / AO)
+    st.start(0u, 0u, kp.key0, kp.key1, rng);
     const long long t_start = kp.trace ? wall_clock64() : 0;
     unsigned rounds = 0, ntasks = 0;
 #if RT_QSTATS
-    // diagnostic build only: wave-level census of the rounds (lane 0 keeps it)
+    // diagnostic build only: [0] rounds [1] lanes casting [2] lanes BOUNCE
+    // [3] lanes CAMERA [4] task rounds [5] lanes taking a task; time [8] cast
+    // [9] resolve_hit [10] tasks [11] next_ray [12] finish
     unsigned long long qs[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tq = __builtin_amdgcn_s_memtime();
 #define QT(slot)                                                   \
@@ -1825,123 +2089,178 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
 #else
 #define QT(slot)
 #endif
-    // A camera ray computed ahead (origin, direction) lives in pf; pf_hi is
-    // the last sample of the task whose ray is computed (in flight or in pf).
-    int pf_hi = -1;
-    double* pf = pf_lds + threadIdx.x;
-    const bool prefetch = RT_PREFETCH && kp.B > 0;
-    while (L.state != SM_DONE) {
+    while (true) {
         ++rounds;
-        if (L.state == SM_CAM && L.s < s1 && pf_hi >= L.s)      // path done, next sample's ray is ready
-            L.begin(kp, pixel, lds_get(pf, 0), lds_get(pf, 3), rng, acc, cnt);
-        QT(12)                       // begin from a prefetched ray
-        const unsigned long long live = __ballot(1), wait = __ballot(L.state == SM_CAM);
-        // lanes with no ray ready for their next path
-        const unsigned long long lack = __ballot(prefetch && L.state == SM_CAST && pf_hi <= L.s && L.s + 1 < s1);
-        const bool go = wait == live || (__popcll(wait) + __popcll(lack)) * 8 >= __popcll(live) * RT_QUEUE_FILL;
-        const bool need = go && L.state == SM_CAM && L.s >= s1;
+#if RT_QSTATS
+        qs[0] += 1;
+        qs[1] += (unsigned long long)__popcll(__ballot(L.state == SM_CAST));
+#endif
+        // ---- 1. closest hit (main.c:52-92) for every lane with a ray ------
+        if (L.state == SM_CAST) {
+            Cnt cnt;
+            L.kind = closest_hit<false, false>(kp, L.o, L.cast_dir(), L.best, L.win, cnt);
+            L.state = SM_RESOLVE;
+        }
+        QT(8)
+        // ---- 2. the hit, up to the next direction --------------------------
+        int role = ROLE_NONE;
+        if (L.state == SM_RESOLVE) role = L.resolve_hit(kp, acc);
+        QT(9)
+        // ---- 3. lanes whose task is done take the next one -----------------
+        const bool need = L.state == SM_CAM && L.s >= s1;
         const unsigned long long nm = __ballot(need);
-        unsigned t = 0;
         if (nm) {                    // wave-uniform: tasks for the lanes that need one
-            const unsigned n = (unsigned)__popcll(nm), avail = qe - qb;
+#if RT_QSTATS
+            qs[4] += 1;
+            qs[5] += (unsigned long long)__popcll(nm);
+#endif
+            unsigned t = 0;
+            const unsigned nn = (unsigned)__popcll(nm), avail = qe - qb;
             const unsigned rank = (unsigned)__popcll(nm & ((1ull << lane) - 1ull));
-            if (avail < n) {         // a new batch (n <= 64 <= RT_QUEUE): old tasks first
+            if (avail < nn) {        // a new batch (nn <= 64 <= RT_QUEUE): old tasks first
                 unsigned nb = 0;
                 if (lane == __ffsll((long long)nm) - 1) nb = atomicAdd(kp.task_ctr, (unsigned)RT_QUEUE);
                 nb = __shfl(nb, __ffsll((long long)nm) - 1, 64);
                 t = rank < avail ? qb + rank : nb + (rank - avail);
-                qb = nb + (n - avail);
+                qb = nb + (nn - avail);
                 qe = nb + RT_QUEUE;
             } else {
                 t = qb + rank;
-                qb += n;
+                qb += nn;
             }
-        }
-        QT(13)                       // ballots, batch grab
-        if (need) {
-            ++ntasks;
-            if (owns) {              // task done: its sums to the chunk partials
-                double* q = kp.partial + ((size_t)chunk * npx + p) * 9;
+            if (need) {
+                ++ntasks;
+                if (owns) {          // task done: its sums to the chunk partials
+                    double* q = kp.partial + ((size_t)chunk * npx + p) * 9;
 #pragma unroll
-                for (int j = 0; j < 9; ++j) q[j] = acc[j * 256];
-                owns = false;
-            }
-            if (t >= ntask) {
-                L.state = SM_DONE;
-            } else {
-                // task t = (chunk, pixel p of the band): launch-constant divisors
-                chunk = udiv_q(t, npx_here, kp.qm_npx, p);
-                unsigned xr;
-                const unsigned row = udiv_q(p, (unsigned)kp.W, kp.qm_w, xr);
-                const int ly = kp.band_y0 + (int)row;
-                x = (int)xr;
-                bool valid = ly < kp.local_rows;
-                if (valid) {
-                    unsigned yy;
-                    const int lt = (int)udiv_q((unsigned)ly, (unsigned)kp.tile_rows, kp.qm_tile, yy);
-                    g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + (int)yy;
-                    valid = g < kp.row_end;
+                    for (int j = 0; j < 9; ++j) q[j] = acc[j * 256];
+                    owns = false;
                 }
-                if (valid) {         // otherwise the lane takes its next task next time
-                    pixel = (uint32_t)g * (uint32_t)kp.W + (uint32_t)x;
-                    L.s = chunk_start(kp, chunk);
-                    s1 = chunk_start(kp, chunk + 1u);
-#pragma unroll
-                    for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
-                    owns = true;
-                    pf_hi = L.s - 1;
-                }
-            }
-        }
-        QT(8)                        // task hand-out
-        if (go) {                    // one camera ray per lane: its next path's, or one ahead
-            const bool now = L.state == SM_CAM && L.s < s1;
-            const bool pre = prefetch && L.state == SM_CAST && pf_hi < min(L.s + 1, s1 - 1);
-#if RT_QSTATS
-            qs[2] += 1;                                         // event rounds
-            qs[3] += (unsigned long long)__popcll(__ballot(now || pre));   // lanes computing a camera ray
-#endif
-            if (now && !prefetch) {
-                L.start(kp, x, g, pixel, s1, rng, acc, cnt);
-            } else if (now || pre) {
-                const int cs = now ? L.s : pf_hi + 1;
-                CamDraws w{philox4x32_10(0u, 0u, pixel, (uint32_t)(kp.s_base + cs), kp.key0, kp.key1), 0};
-                V3 no, rd;
-                camera_ray<false>(kp, x, g, w, no, rd);
-                pf_hi = cs;
-                if (now) {
-                    L.begin(kp, pixel, no, rd, rng, acc, cnt);
+                if (t >= ntask) {
+                    L.state = SM_DONE;
                 } else {
-                    lds_put(pf, 0, no);
-                    lds_put(pf, 3, rd);
+                    // task t = (chunk, pixel p of the band): launch-constant divisors
+                    chunk = udiv_q(t, npx_here, kp.qm_npx, p);
+                    unsigned xr;
+                    const unsigned row = udiv_q(p, (unsigned)kp.W, kp.qm_w, xr);
+                    const int ly = kp.band_y0 + (int)row;
+                    x = (int)xr;
+                    bool valid = ly < kp.local_rows;
+                    if (valid) {
+                        unsigned yy;
+                        const int lt = (int)udiv_q((unsigned)ly, (unsigned)kp.tile_rows, kp.qm_tile, yy);
+                        g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + (int)yy;
+                        valid = g < kp.row_end;
+                    }
+                    if (valid) {     // otherwise the lane takes its next task next round
+                        pixel = (uint32_t)g * (uint32_t)kp.W + (uint32_t)x;
+                        L.s = chunk_start(kp, chunk);
+                        s1 = chunk_start(kp, chunk + 1u);
+#pragma unroll
+                        for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
+                        owns = true;
+                    }
                 }
             }
         }
+        if (__ballot(L.state != SM_DONE) == 0ull) break;     // every lane of the wave is done
+        // tracer with nbRebondMax <= 0 returns (0, 0, 0) albedo/normal/colour
+        if (kp.B <= 0 && L.state == SM_CAM && L.s < s1) {
+            acc_add(acc, ACC_ALB, v3(0, 0, 0));
+            acc_add(acc, ACC_NRM, v3(0, 0, 0));
+            acc_add(acc, ACC_RAD, v3(0, 0, 0));
+            ++L.s;
+            continue;
+        }
+        if (L.state == SM_CAM && L.s < s1) role = ROLE_CAMERA;
+        QT(10)
 #if RT_QSTATS
-        {
-            const unsigned long long c = __ballot(L.state == SM_CAST);
-            qs[0] += 1;                                         // rounds
-            qs[1] += (unsigned long long)__popcll(c);           // lanes casting
-            qs[4] += (unsigned long long)__popcll(__ballot(L.state == SM_CAM));    // lanes waiting
-            qs[7] += c ? 1 : 0;                                 // rounds with a cast
-        }
-        QT(9)                        // camera-ray events (every QT outside divergent code)
-        if (L.state == SM_CAST) L.cast_flat(kp, cnt);
-        QT(10)                       // cast
-        L.dbg_lit = false;
-        if (L.state == SM_RESOLVE) L.resolve(kp, acc, cnt);
-        QT(11)                       // resolve
-        {
-            const unsigned long long lm = __ballot(L.dbg_lit);
-            qs[6] += lm ? 1 : 0;                                // rounds with a lit (HSL) lane
-            qs[5] += (unsigned long long)__popcll(lm);          // lit lanes
-        }
-#else
-        if (L.state == SM_CAST) {
-            L.cast_flat(kp, cnt);
-            L.resolve(kp, acc, cnt);
-        }
+        qs[2] += (unsigned long long)__popcll(__ballot(role == ROLE_BOUNCE));
+        qs[3] += (unsigned long long)__popcll(__ballot(role == ROLE_CAMERA));
 #endif
+        // ---- 4. next ray: bounce direction or camera ray (shared work) ----
+        if (role != ROLE_NONE) {
+            const bool cam = role == ROLE_CAMERA;
+            // draws: a bounce uses draws n, n+1 of its sample (rtutility.h:
+            // 189-203); a camera ray draws 0-3 of sample s (main.c:265-269)
+            const uint32_t nd = cam ? 0u : st.n;
+            const uint32_t sa = nd & 3u, sb = (nd + 1u) & 3u;
+            uint32_t wa = 0, wb = 0;
+            if (!cam && sa != 0u) wa = rng[sa * 256];          // cached word of the current block
+            if (!cam && sb != 0u && sa != 0u) wb = rng[sb * 256];
+            Philox blk{0, 0, 0, 0};
+            if (cam || sa == 0u || sb == 0u) {                 // a new block: one Philox for both roles
+                const uint32_t bi = cam ? 0u : ((nd + (sa == 0u ? 0u : 1u)) >> 2);
+                blk = philox4x32_10(bi, 0u, pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1);
+                if (!cam) {                                     // keep the rest of the block
+                    rng[256] = blk.w1;
+                    rng[512] = blk.w2;
+                    rng[768] = blk.w3;
+                }
+            }
+            if (!cam) {
+                if (sa == 0u) wa = blk.w0;
+                if (sb == 0u) wb = blk.w0;
+                else if (sa == 0u) wb = blk.w1;
+            }
+            V3 X;
+            V3 no = v3(0, 0, 0);
+            if (cam) {
+                CamDraws w{blk, 0};
+                const double ju = -0.5 + 1.0 * unit31(w.next31());     // randomDouble(-0.5, 0.5)
+                const double jv = -0.5 + 1.0 * unit31(w.next31());
+                const double jx = -0.5 + 1.0 * unit31(w.next31());
+                const double jy = -0.5 + 1.0 * unit31(w.next31());
+                const int b = opq0();
+                const cdptr U = (cdptr)kp.uni;
+                const double nu = (double)x + ju, nv = (double)g + jv;
+                const double rcw = U[b + U_RC_WM1], rch = U[b + U_RC_HM1];
+                const double u = rcw != 0.0 ? div_core(nu, U[b + U_WM1], rcw) : nu / U[b + U_WM1];
+                const double v = rch != 0.0 ? div_core(nv, U[b + U_HM1], rch) : nv / U[b + U_HM1];
+                const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
+                const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
+                const V3 ch = v3(U[b + U_CAM_H], U[b + U_CAM_H + 1], U[b + U_CAM_H + 2]);
+                const V3 cv = v3(U[b + U_CAM_V], U[b + U_CAM_V + 1], U[b + U_CAM_V + 2]);
+                const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
+                const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));     // get_ray, camera.h:42-55
+                const V3 dest = co + muls(dir, U[b + U_FOCUS]);
+                no = co + v3(dx, dy, 0);
+                X = dest - no;
+            } else {
+                // random_dir_no_norm (rtutility.h:189-203), then n + dir (main.c:163)
+                const double u = unit31(wa >> 1);
+                const double v = unit31(wb >> 1);
+                const double theta = 0x1.921fb54442d18p+2 * u;        // 2*PI*u
+                const double xv = 2 * v - 1;                          // phi = acos(2v - 1)
+                float st_, ct_, sp_, cp_;
+                if (!phi_sincosf_fast(xv, sp_, cp_)) {
+                    const double phi = pm_acos(xv);
+                    pm_sincosf((float)phi, sp_, cp_);
+                }
+                pm_sincosf((float)theta, st_, ct_);
+                X = L.hn + normalize(v3((double)(ct_ * sp_), (double)(st_ * sp_), (double)cp_));
+                st.n += 2;
+            }
+            const V3 dn = normalize(X);
+            QT(11)
+            if (cam) {                                         // the new sample's primary ray
+                L.o = no;
+                L.d = dn;
+                if (AOM == AO_ON) L.cd = dn;
+                L.inc = v3(0, 0, 0);
+                L.rc = v3(1, 1, 1);
+                L.top_n2 = 1.0;
+                L.i = 0;
+                L.chain = true;
+                L.ao_cast = false;
+                L.state = SM_CAST;
+                st.start(pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1, rng);
+                st.n = 4;                                      // draws 0-3 were the camera's
+            } else {
+                L.finish_bounce(kp, dn, st, acc);
+            }
+        }
+        QT(12)
     }
     if (kp.trace) {                  // diagnostics (RT_QUEUE_TRACE): per lane start, end, rounds, tasks
         unsigned long long* q = kp.trace + ((size_t)blockIdx.x * 256 + threadIdx.x) * RT_TRACE_WORDS;
@@ -2142,16 +2461,37 @@ static dim3 grid_for(const KParams& kp)
 // are compiled only into the variants that use them, so a sphere-only scene
 // runs a kernel without their registers.
 template <bool COUNT>
-static void launch_variant(const KParams& kp, void* stream)
+static void launch_variant(const KParams& kp_in, void* stream)
 {
-    const dim3 g = grid_for(kp);
+    const dim3 g = grid_for(kp_in);
     const hipStream_t st = (hipStream_t)stream;
+    KParams kp = kp_in;
+#if RT_QSTATS
+    // diagnostic build: samples_coop's census summed into 16 counters, appended to RT_QUEUE_TRACE
+    const char* tf = COUNT ? nullptr : std::getenv("RT_QUEUE_TRACE");
+    if (tf && kp.bvh) {
+        (void)hipMalloc((void**)&kp.trace, 16 * sizeof(unsigned long long));
+        (void)hipMemsetAsync(kp.trace, 0, 16 * sizeof(unsigned long long), st);
+    }
+#endif
     if (kp.cuda && kp.bvh) hipLaunchKernelGGL((render_kernel_cuda<COUNT, true>), g, dim3(256), 0, st, kp);
     else if (kp.cuda) hipLaunchKernelGGL((render_kernel_cuda<COUNT, false>), g, dim3(256), 0, st, kp);
     else if (kp.bvh && kp.sky) hipLaunchKernelGGL((render_kernel<COUNT, true, true>), g, dim3(256), 0, st, kp);
     else if (kp.bvh) hipLaunchKernelGGL((render_kernel<COUNT, true, false>), g, dim3(256), 0, st, kp);
     else if (kp.sky) hipLaunchKernelGGL((render_kernel<COUNT, false, true>), g, dim3(256), 0, st, kp);
     else hipLaunchKernelGGL((render_kernel<COUNT, false, false>), g, dim3(256), 0, st, kp);
+#if RT_QSTATS
+    if (kp.trace) {
+        unsigned long long h[16];
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpy(h, kp.trace, sizeof h, hipMemcpyDeviceToHost);
+        (void)hipFree(kp.trace);
+        if (FILE* f = std::fopen(tf, "ab")) {
+            std::fwrite(h, sizeof(unsigned long long), 16, f);
+            std::fclose(f);
+        }
+    }
+#endif
 }
 
 #if RT_QUEUE > 0

@@ -34,15 +34,15 @@ torch.cuda.synchronize()
 del os.environ["RT_QUEUE_TRACE"]
 d = np.fromfile(path, dtype=np.uint64).reshape(-1, 18)
 w = d[::64]                                  # lane 0 of each wave holds the wave census
-q = w[:, 4:12].astype(np.float64)
-t = w[:, 12:18].astype(np.float64).sum(0)
+q = w[:, 4:18].astype(np.float64)
 tot = q.sum(0)
-rounds, cast_l, ev, ev_l, wait_l, done_l, task_r, cast_r = tot
+rounds, cast_l, bounce_l, cam_l, task_r, task_l = tot[:6]
+t = tot[8:13]
 res = {"spp": spp, "scene": kind, "waves": int(len(w)), "rounds_per_wave": rounds / len(w),
-       "cast_lane_util": cast_l / (64 * cast_r), "rounds_with_cast_frac": cast_r / rounds,
-       "event_rounds_frac": ev / rounds, "event_lane_util": ev_l / (64 * ev),
-       "wait_lane_frac": wait_l / (64 * rounds), "lit_lanes_per_lit_round": done_l / max(task_r, 1),
-       "lit_rounds_frac": task_r / rounds,
-       "time_share": {k: round(v / t.sum(), 4) for k, v in zip(("task", "events", "cast", "resolve", "begin", "ballots"), t)},
-       "lane_casts_total": cast_l, "samples": 1200 * 900 * spp, "casts_per_sample": cast_l / (1200 * 900 * spp)}
+       "cast_lane_util": cast_l / (64 * rounds), "bounce_lanes_per_round": bounce_l / rounds,
+       "camera_lanes_per_round": cam_l / rounds, "task_rounds_frac": task_r / rounds,
+       "tasks_per_task_round": task_l / max(task_r, 1),
+       "time_share": {k: round(v / t.sum(), 4) for k, v in zip(("cast", "resolve_hit", "tasks", "next_ray",
+                                                                 "finish"), t)},
+       "samples": 1200 * 900 * spp, "casts_per_sample": cast_l / (1200 * 900 * spp)}
 print(json.dumps(res))
