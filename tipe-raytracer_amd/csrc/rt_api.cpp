@@ -144,6 +144,7 @@ struct rt_device_scene {
     int* tri_orig = nullptr;         // leaf order -> caller's triangle index
     int bvh_nodes = 0, bvh_depth = 0;
     double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0;
+    float bvh_rbox = 0.0f;           // >= every |bound| of the BVH's boxes
     bool mats_bounded = false;       // every diffuse/emission/strength finite, |x| <= 2^100
     double coord_max = HUGE_VAL;     // max |coordinate| of the spheres (|C_a| + R) and triangle vertices
 };
@@ -280,6 +281,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
         kp.bvh = sc->bvh;
         kp.bvh_srel = sc->s_rel;
         kp.bvh_sabs = sc->s_abs;
+        kp.bvh_rbox = sc->bvh_rbox;
     }
     return RT_OK;
 }
@@ -687,6 +689,14 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->s_rel = bvh.s_rel;
     ds->s_abs = bvh.s_abs;
     ds->r_scene = bvh.r_scene;
+    {
+        float rb = 0.0f;             // the single-precision slab margin's coordinate bound
+        for (const BvhNode4& nd : bvh.nodes4)
+            for (int c = 0; c < 4; ++c)
+                if (nd.count[c] >= 0)
+                    for (int a = 0; a < 3; ++a) rb = std::max({rb, std::fabs(nd.lo[a][c]), std::fabs(nd.hi[a][c])});
+        ds->bvh_rbox = std::isfinite(rb) ? rb * (1.0f + 0x1p-20f) : HUGE_VALF;
+    }
     if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_cand, cand)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
         (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels)) ||
         (rc = upload(&ds->bvh, bvh.nodes4)) || (rc = upload(&ds->tri_orig, bvh.order)) ||

@@ -82,6 +82,7 @@ struct KParams {
     const double* sph_rinv;  // 1/radius per sphere (sphere_uvmapping's divide)
     int sky_w, sky_h;
     double bvh_srel, bvh_sabs;   // distance-cull slack (rt_bvh.cpp)
+    float bvh_rbox;              // >= |every bound| of the tree's boxes (single-precision slab margin)
     int ns, ns_pad, nt;
     int tw, th;
     long long n_texels;

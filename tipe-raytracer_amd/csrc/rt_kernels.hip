@@ -465,12 +465,61 @@ __device__ __forceinline__ unsigned short* bvh_stack()
     __shared__ unsigned short stk_lds[kStack4 * 256];
     return stk_lds + threadIdx.x;
 }
-__device__ __forceinline__ V3 bvh_inv(const V3 d)
+// Conservative single-precision slab test (the culling only has to be a
+// superset of the double test on the padded boxes).  Per ray
+// and axis: inv = rcp((float)d) (|d| clamped to >= 2^-60; <= 2 ulp of 1/d),
+// and two offsets a, b = -(float)o * inv -/+ s E with s = sign(inv) and
+//   E = 2^-19 (rbox + |(float)o|) |inv|,
+// rbox >= every |bound| of the tree.  The near and far slab distances
+// fma(lo, inv, a) and fma(hi, inv, b) then lie below / above the exact
+// (bound - o) / d: the rounding of d, o, inv, o*inv, the offsets and the fma
+// together stay within 6 u (rbox + |o|) |inv| + 2 u E < E / 5 (u = 2^-24).
+// The cull thresholds are rounded outward in the same way.
+struct Ray32 {
+    float ix, iy, iz;            // ~1/d
+    float ax, ay, az;            // offsets of the lo bounds
+    float bx, by, bz;            // offsets of the hi bounds
+};
+__device__ __forceinline__ void ray32_axis(double oc, double dc, float rbox, float& inv, float& a, float& b)
 {
-    const double lim = 0x1p-200;
-    return v3(1.0 / (fabs(d.x) < lim ? copysign(lim, d.x) : d.x),
-              1.0 / (fabs(d.y) < lim ? copysign(lim, d.y) : d.y),
-              1.0 / (fabs(d.z) < lim ? copysign(lim, d.z) : d.z));
+    const double lim = 0x1p-60;
+    const float df = (float)(fabs(dc) < lim ? copysign(lim, dc) : dc);
+    inv = __builtin_amdgcn_rcpf(df);
+    const float of = (float)oc;
+    const float oi = of * inv;
+    const float E = 0x1p-19f * ((rbox + fabsf(of)) * fabsf(inv));
+    const float sE = inv >= 0.0f ? E : -E;
+    a = -oi - sE;
+    b = -oi + sE;
+}
+__device__ __forceinline__ Ray32 ray32(const V3 o, const V3 d, float rbox)
+{
+    Ray32 r;
+    ray32_axis(o.x, d.x, rbox, r.ix, r.ax, r.bx);
+    ray32_axis(o.y, d.y, rbox, r.iy, r.ay, r.by);
+    ray32_axis(o.z, d.z, rbox, r.iz, r.az, r.bz);
+    return r;
+}
+// float(best * srel + sabs) rounded up (the triangle test's distance cull)
+__device__ __forceinline__ float cull32(const KParams& kp, double best)
+{
+    return (float)fma(best, 1.0 + kp.bvh_srel, kp.bvh_sabs) * (1.0f + 0x1p-22f);
+}
+// The four child boxes of a node: hit flags and near distances.
+__device__ __forceinline__ void box4(const KParams& kp, const BvhNode4* nd, const Ray32& r, float cull, bool h[4],
+                                     float tn[4])
+{
+    const float nsabs = (float)(-kp.bvh_sabs) * (1.0f + 0x1p-22f);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float x0 = fmaf(nd->lo[0][c], r.ix, r.ax), x1 = fmaf(nd->hi[0][c], r.ix, r.bx);
+        const float y0 = fmaf(nd->lo[1][c], r.iy, r.ay), y1 = fmaf(nd->hi[1][c], r.iy, r.by);
+        const float z0 = fmaf(nd->lo[2][c], r.iz, r.az), z1 = fmaf(nd->hi[2][c], r.iz, r.bz);
+        const float tmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
+        const float tmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+        h[c] = nd->count[c] >= 0 && tmin <= tmax && tmax >= nsabs && tmin <= cull;
+        tn[c] = tmin;
+    }
 }
 
 // One node visit: the four child boxes, the triangles of the hit leaves, then
@@ -478,30 +527,20 @@ __device__ __forceinline__ V3 bvh_inv(const V3 d)
 // false when the traversal is over.  tris_bvh loops it to the end; the
 // resumable trace (render_sm) runs a bounded number of visits per round.
 template <bool COUNT, bool CU>
-__device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3 d, const V3 inv,
+__device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3 d, const Ray32& r32,
                                          unsigned short* stk, int& node, int& sp, double& best, int& kind,
                                          int& win, int& win_orig, Cnt& cnt)
 {
-    const double srel = 1.0 + kp.bvh_srel, sabs = kp.bvh_sabs;
     const BvhNode4* nd = kp.bvh + node;
     if (COUNT) {
         cnt.c[RT_CNT_BVH_NODES] += 1;
         wave_slots(cnt, RT_CNT_BVH_LANE_SLOTS);
     }
     bool h[4];
-    double tn[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const double x0 = ((double)nd->lo[0][c] - o.x) * inv.x, x1 = ((double)nd->hi[0][c] - o.x) * inv.x;
-        const double y0 = ((double)nd->lo[1][c] - o.y) * inv.y, y1 = ((double)nd->hi[1][c] - o.y) * inv.y;
-        const double z0 = ((double)nd->lo[2][c] - o.z) * inv.z, z1 = ((double)nd->hi[2][c] - o.z) * inv.z;
-        const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
-        const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
-        h[c] = nd->count[c] >= 0 && tmin <= tmax && tmax >= -sabs && tmin <= best * srel + sabs;
-        tn[c] = tmin;
-    }
+    float tn[4];
+    box4(kp, nd, r32, cull32(kp, best), h, tn);
     int next = -1;
-    double tnext = 0.0;
+    float tnext = 0.0f;
     unsigned lm = 0;                                     // hit leaf slots
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -562,9 +601,9 @@ __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3
                                          int& win, int& win_orig, Cnt& cnt)
 {
     unsigned short* stk = bvh_stack();
-    const V3 inv = bvh_inv(d);
+    const Ray32 r32 = ray32(o, d, kp.bvh_rbox);
     int node = 0, sp = 0;
-    while (bvh_step<COUNT, CU>(kp, o, d, inv, stk, node, sp, best, kind, win, win_orig, cnt)) {
+    while (bvh_step<COUNT, CU>(kp, o, d, r32, stk, node, sp, best, kind, win, win_orig, cnt)) {
     }
 }
 
@@ -1104,7 +1143,8 @@ template <bool COUNT, bool SKY, int AOM = AO_RUNTIME>
 struct LanePath {
     Stream st;
     V3 o, d, cd;                                 // ray, next bounce direction, current cast's direction
-    V3 inc, rc, inv;
+    V3 inc, rc;
+    Ray32 r32;                                   // the cast's single-precision slab set-up (BVH)
     double top_n2, best;
     int i, kind, win, win_orig, node, sp, s, state;
     bool chain, ao_cast;
@@ -1130,7 +1170,8 @@ struct LanePath {
 
     __device__ __forceinline__ void init(int s0, int s1)
     {
-        o = d = cd = inc = rc = inv = v3(0, 0, 0);
+        o = d = cd = inc = rc = v3(0, 0, 0);
+        r32 = Ray32{0, 0, 0, 0, 0, 0, 0, 0, 0};
         top_n2 = 1.0;
         best = 0.0;
         i = 0; kind = HIT_NONE; win = -1; win_orig = 0; node = 0; sp = 0;
@@ -1352,7 +1393,7 @@ struct LanePath {
         win = cast_spheres<COUNT, false>(kp, o, cd, best, cnt);
         kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
         win_orig = 0;
-        inv = bvh_inv(cd);
+        if (kp.bvh) r32 = ray32(o, cd, kp.bvh_rbox);
         node = 0;
         sp = 0;
         state = SM_TRAV;
@@ -1363,7 +1404,7 @@ struct LanePath {
     {
 #pragma unroll 1
         for (int j = 0; j < k; ++j) {
-            if (!bvh_step<COUNT, false>(kp, o, cd, inv, stk, node, sp, best, kind, win, win_orig, cnt)) {
+            if (!bvh_step<COUNT, false>(kp, o, cd, r32, stk, node, sp, best, kind, win, win_orig, cnt)) {
                 state = SM_RESOLVE;
                 break;
             }
@@ -1474,31 +1515,21 @@ __device__ __forceinline__ void lifo_push(volatile unsigned* q, int& cnt, int n,
 // children other than the next one go to push[] (for the LIFO) when
 // to_lifo, else on the lane's own stack.  hit: a triangle beat the record.
 template <bool COUNT>
-__device__ __forceinline__ bool coop_step(const KParams& kp, const V3 o, const V3 d, const V3 inv,
+__device__ __forceinline__ bool coop_step(const KParams& kp, const V3 o, const V3 d, const Ray32& r32,
                                           unsigned short* stk, int& node, int& sp, double& best, int& kind,
                                           int& win, int& win_orig, bool& hit, bool to_lifo, unsigned* push,
                                           int& npush, Cnt& cnt)
 {
-    const double srel = 1.0 + kp.bvh_srel, sabs = kp.bvh_sabs;
     const BvhNode4* nd = kp.bvh + node;
     if (COUNT) {
         cnt.c[RT_CNT_BVH_NODES] += 1;
         wave_slots(cnt, RT_CNT_BVH_LANE_SLOTS);
     }
     bool h[4];
-    double tn[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const double x0 = ((double)nd->lo[0][c] - o.x) * inv.x, x1 = ((double)nd->hi[0][c] - o.x) * inv.x;
-        const double y0 = ((double)nd->lo[1][c] - o.y) * inv.y, y1 = ((double)nd->hi[1][c] - o.y) * inv.y;
-        const double z0 = ((double)nd->lo[2][c] - o.z) * inv.z, z1 = ((double)nd->hi[2][c] - o.z) * inv.z;
-        const double tmin = fmax(fmax(fmin(x0, x1), fmin(y0, y1)), fmin(z0, z1));
-        const double tmax = fmin(fmin(fmax(x0, x1), fmax(y0, y1)), fmax(z0, z1));
-        h[c] = nd->count[c] >= 0 && tmin <= tmax && tmax >= -sabs && tmin <= best * srel + sabs;
-        tn[c] = tmin;
-    }
+    float tn[4];
+    box4(kp, nd, r32, cull32(kp, best), h, tn);
     int next = -1;
-    double tnext = 0.0;
+    float tnext = 0.0f;
     unsigned lm = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -1618,7 +1649,8 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
         }
         bool has = false;
         int tr = 0, tnode = 0, tsp = 0;
-        V3 to = v3(0, 0, 0), td = to, tinv = to;
+        V3 to = v3(0, 0, 0), td = to;
+        Ray32 tr32 = Ray32{0, 0, 0, 0, 0, 0, 0, 0, 0};
         for (;;) {
 #if RT_QSTATS
             qs[2] += 1;
@@ -1651,7 +1683,7 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
                 if (fresh) {
                     to = ro;
                     td = rd;
-                    tinv = bvh_inv(rd);
+                    tr32 = ray32(ro, rd, kp.bvh_rbox);
                 }
             }
             double best = shfl_d(L.best, tr);
@@ -1661,7 +1693,7 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
             int npush = 0;
             const bool to_lifo = qn < 64;
             if (has) {
-                if (!coop_step<COUNT>(kp, to, td, tinv, stk, tnode, tsp, best, kind, win, win_orig, hit, to_lifo,
+                if (!coop_step<COUNT>(kp, to, td, tr32, stk, tnode, tsp, best, kind, win, win_orig, hit, to_lifo,
                                       push, npush, cnt))
                     has = false;
 #pragma unroll
