@@ -334,6 +334,14 @@ int rt_verify_sampler_phi(unsigned long long r0, unsigned long long n, unsigned 
  * device 0. */
 int rt_verify_sphere_pass(const rt_scene* scene, const double* rays, long long n, unsigned long long counts[2]);
 
+/* Stress check of the kernel's normalize (vec3.h:137-139, a / sqrt(a.a)):
+ * n pseudo-random vectors (Philox keyed by seed; unit-scale, n + dir sums,
+ * common and per-component binary scales 2^-450..2^450) through the fast
+ * exact path against the IEEE sqrt and divisions.  counts[0] = vectors on the
+ * fast path, counts[1] = results that differ in any bit (0 is the
+ * correctness bar).  Synchronous, device 0. */
+int rt_verify_normalize(unsigned long long seed, unsigned long long n, unsigned long long counts[2]);
+
 #ifdef __cplusplus
 }
 #endif

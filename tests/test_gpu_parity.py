@@ -114,6 +114,15 @@ def test_device_normalize_fast_path_is_ieee():
     assert same.all(), v[~same.all(1)][:4]
 
 
+def test_device_normalize_stress():
+    """normalize()'s fast path (sqrt_rcp_core: 1/|a| refined from the sqrt
+    sequence's rsq, then div_core) equals IEEE a / sqrt(a.a) bit for bit on
+    2^32 pseudo-random vectors (directions, n + dir sums, scales 2^-450..2^450)."""
+    fast, bad = tipe_rt.verify_normalize(seed=20261016, n=1 << 32)
+    assert bad == 0
+    assert fast > (1 << 31)
+
+
 def test_sampler_phi_fast_path_exhaustive():
     """The fast phi path (phi_sincosf_fast) gives the full path's floats for
     every one of the 2^31 rand() values, and falls back rarely."""

@@ -1126,4 +1126,28 @@ int rt_verify_sampler_phi(unsigned long long r0, unsigned long long n, unsigned 
     return RT_OK;
 }
 
+int rt_verify_normalize(unsigned long long seed, unsigned long long n, unsigned long long counts[2])
+{
+    if (!counts) return fail(RT_EINVAL, "verify_normalize: counts is NULL");
+    counts[0] = counts[1] = 0;
+    if (n == 0) return RT_OK;
+    int dev = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        int rc = ensure_init_locked();
+        if (rc) return rc;
+        dev = g_devices[0];
+    }
+    DeviceGuard guard(dev);
+    unsigned long long* d = nullptr;
+    HIP_TRY(hipMalloc((void**)&d, 2 * sizeof(unsigned long long)));
+    hipError_t e = hipMemset(d, 0, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = (hipError_t)launch_verify_normalize(seed, n, d);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(counts, d, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(RT_EDEVICE, "verify_normalize: %s", hipGetErrorString(e));
+    return RT_OK;
+}
+
 }  // extern "C"

@@ -220,6 +220,26 @@ __device__ __forceinline__ double sqrt_core(double x)          // x in [2^-760, 
     g = fma(fma(-g, g, x), h, g);
     return fma(fma(-g, g, x), h, g);
 }
+// sqrt_core(x) and a refined reciprocal of that root for div_core, without
+// v_rcp_f64: the sqrt sequence's own h ~ 1/(2 sqrt x) (relative error
+// ~1.5 e0^2 <= 2^-45 after its Goldschmidt step, e0 <= 2^-23.5 the error of
+// v_rsq_f64) doubled is within 2^-45 of 1/L (L = the rounded root, itself
+// within 2^-53 of sqrt x), and one Newton step on it, as rcp_refined's
+// second step, leaves rc within 2^-89 + half an ulp of 1/L.  Same
+// precondition for div_core as rcp_refined's result; rt_verify_normalize
+// compares normalize() with IEEE a / sqrt(a.a) on 2^33 random vectors.
+__device__ __forceinline__ void sqrt_rcp_core(double x, double& L, double& rc)   // x in [2^-760, 2^760]
+{
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    g = fma(fma(-g, g, x), h, g);
+    L = fma(fma(-g, g, x), h, g);
+    const double r0 = h + h;
+    rc = fma(r0, fma(-L, r0, 1.0), r0);
+}
 __device__ __forceinline__ double rcp_refined(double d)         // d in [2^-400, 2^400]
 {
     double rc = __builtin_amdgcn_rcp(d);

@@ -122,6 +122,7 @@ int launch_assemble(const double* gathered, long long rank_stride, int world, in
                     int rows_per_rank, int W, int H, double* out, void* stream);
 int launch_selftest(int op, const double* d_in, double* d_out, int n, void* stream);
 int launch_verify_phi(unsigned long long r0, unsigned long long n, unsigned long long* d_counts);
+int launch_verify_normalize(unsigned long long seed, unsigned long long n, unsigned long long* d_counts);
 int launch_verify_spheres(const KParams& kp, const double* d_rays, long long n, unsigned long long* d_counts);
 int launch_resolve(const KParams& kp, void* stream);
 int launch_denoise_pack(long long npx, const double* canva, const double* albedo, const double* normal,

@@ -39,6 +39,7 @@
 //    in chunk order by combine_kernel (a deterministic, GPU-count-independent
 //    grouping that the oracle reproduces).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
@@ -96,6 +97,9 @@ static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) m
 #define RT_QSTATS 0
 #endif
 #define RT_TRACE_WORDS (RT_QSTATS ? 18 : 4)
+#ifndef RT_NRM_RSQ                  // normalize: 1/|a| refined from the sqrt sequence's own rsq (no v_rcp_f64)
+#define RT_NRM_RSQ 1
+#endif
 #ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
 #define RT_WAVES_PER_SIMD_BVH 3
 #endif
@@ -125,11 +129,29 @@ __device__ __forceinline__ V3 normalize(V3 a)
     const double n2 = dot(a, a);
     const double mn = fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
     if (n2 >= 0x1p-760 && n2 <= 0x1p760 && mn >= 0x1p-900) {
+#if RT_NRM_RSQ
+        double L, rc;
+        sqrt_rcp_core(n2, L, rc);
+#else
         const double L = sqrt_core(n2);
         const double rc = rcp_refined(L);
+#endif
         return v3(div_core(a.x, L, rc), div_core(a.y, L, rc), div_core(a.z, L, rc));
     }
     return divs(a, sqrt(n2));
+}
+
+// The kernel's by-value parameters (kernarg segment) through an address the
+// compiler cannot see through: fields read via it are loaded (s_load) where
+// they are used instead of being held in SGPRs -- and spilled to VGPR lanes,
+// one v_readlane per reload -- across a long loop.
+// (KParams is the only argument of the kernels that use this: offset 0.)
+typedef const __attribute__((address_space(4))) KParams* KParamsK;
+__device__ __forceinline__ KParamsK kp_here()
+{
+    KParamsK p = (KParamsK)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return p;
 }
 
 // Cost-attribution knobs (tools/attribute_costs.sh): RT_DUP_<part> runs a
@@ -1856,13 +1878,13 @@ __device__ __forceinline__ unsigned udiv_q(unsigned n, unsigned d, unsigned m, u
 }
 
 // First sample of chunk c: c*S/P (exact; 32-bit when S*P < 2^32).
-__device__ __forceinline__ int chunk_start(const KParams& kp, unsigned c)
+__device__ __forceinline__ int chunk_start(int S, int chunks, unsigned qm_chunks, unsigned c)
 {
-    if (kp.qm_chunks != 0u) {
+    if (qm_chunks != 0u) {
         unsigned r;
-        return (int)udiv_q(c * (unsigned)kp.S, (unsigned)kp.chunks, kp.qm_chunks, r);
+        return (int)udiv_q(c * (unsigned)S, (unsigned)chunks, qm_chunks, r);
     }
-    return (int)(((long long)c * kp.S) / kp.chunks);
+    return (int)(((long long)c * S) / chunks);
 }
 
 // One lane's path in render_kernel_q: tracer's state (main.c:118-242) for
@@ -2088,9 +2110,6 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     double* acc = acc_lds + threadIdx.x;
     uint32_t* rng = rng_lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
-    const unsigned npx = (unsigned)kp.band_rows * (unsigned)kp.W;     // partials' chunk stride
-    const unsigned npx_here = kp.npx_here;            // pixels of this band that exist
-    const unsigned ntask = npx_here * (unsigned)kp.chunks;
     unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
     QPath<SKY, AOM> L;
     L.o = L.d = L.cd = L.inc = L.rc = L.hn = v3(0, 0, 0);
@@ -2142,6 +2161,9 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
         const bool need = L.state == SM_CAM && L.s >= s1;
         const unsigned long long nm = __ballot(need);
         if (nm) {                    // wave-uniform: tasks for the lanes that need one
+            // launch constants re-read here (SMEM) instead of living in SGPRs
+            // spilled to VGPR lanes across the whole round
+            const KParamsK K = kp_here();
 #if RT_QSTATS
             qs[4] += 1;
             qs[5] += (unsigned long long)__popcll(nm);
@@ -2151,7 +2173,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
             const unsigned rank = (unsigned)__popcll(nm & ((1ull << lane) - 1ull));
             if (avail < nn) {        // a new batch (nn <= 64 <= RT_QUEUE): old tasks first
                 unsigned nb = 0;
-                if (lane == __ffsll((long long)nm) - 1) nb = atomicAdd(kp.task_ctr, (unsigned)RT_QUEUE);
+                if (lane == __ffsll((long long)nm) - 1) nb = atomicAdd(K->task_ctr, (unsigned)RT_QUEUE);
                 nb = __shfl(nb, __ffsll((long long)nm) - 1, 64);
                 t = rank < avail ? qb + rank : nb + (rank - avail);
                 qb = nb + (nn - avail);
@@ -2163,31 +2185,31 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
             if (need) {
                 ++ntasks;
                 if (owns) {          // task done: its sums to the chunk partials
-                    double* q = kp.partial + ((size_t)chunk * npx + p) * 9;
+                    double* q = K->partial + ((size_t)chunk * ((unsigned)K->band_rows * (unsigned)K->W) + p) * 9;
 #pragma unroll
                     for (int j = 0; j < 9; ++j) q[j] = acc[j * 256];
                     owns = false;
                 }
-                if (t >= ntask) {
+                if (t >= K->npx_here * (unsigned)K->chunks) {
                     L.state = SM_DONE;
                 } else {
                     // task t = (chunk, pixel p of the band): launch-constant divisors
-                    chunk = udiv_q(t, npx_here, kp.qm_npx, p);
+                    chunk = udiv_q(t, K->npx_here, K->qm_npx, p);
                     unsigned xr;
-                    const unsigned row = udiv_q(p, (unsigned)kp.W, kp.qm_w, xr);
-                    const int ly = kp.band_y0 + (int)row;
+                    const unsigned row = udiv_q(p, (unsigned)K->W, K->qm_w, xr);
+                    const int ly = K->band_y0 + (int)row;
                     x = (int)xr;
-                    bool valid = ly < kp.local_rows;
+                    bool valid = ly < K->local_rows;
                     if (valid) {
                         unsigned yy;
-                        const int lt = (int)udiv_q((unsigned)ly, (unsigned)kp.tile_rows, kp.qm_tile, yy);
-                        g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + (int)yy;
-                        valid = g < kp.row_end;
+                        const int lt = (int)udiv_q((unsigned)ly, (unsigned)K->tile_rows, K->qm_tile, yy);
+                        g = K->row_base + (K->tile_first + lt * K->tile_step) * K->tile_rows + (int)yy;
+                        valid = g < K->row_end;
                     }
                     if (valid) {     // otherwise the lane takes its next task next round
-                        pixel = (uint32_t)g * (uint32_t)kp.W + (uint32_t)x;
-                        L.s = chunk_start(kp, chunk);
-                        s1 = chunk_start(kp, chunk + 1u);
+                        pixel = (uint32_t)g * (uint32_t)K->W + (uint32_t)x;
+                        L.s = chunk_start(K->S, K->chunks, K->qm_chunks, chunk);
+                        s1 = chunk_start(K->S, K->chunks, K->qm_chunks, chunk + 1u);
 #pragma unroll
                         for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
                         owns = true;
@@ -2680,6 +2702,67 @@ __global__ __launch_bounds__(256) void verify_spheres_kernel(const KParams kp, c
         if (nf) atomicAdd(counts, nf);
         if (nb) atomicAdd(counts + 1, nb);
     }
+}
+
+// normalize() (fast lanes: sqrt_rcp_core / rcp_refined + div_core) against
+// IEEE a / sqrt(a.a) on n pseudo-random vectors (Philox, key = seed): half
+// unit-scale (directions and n + dir sums), a quarter with one common scale
+// 2^e, e in [-400, 400), a quarter with independent per-component scales.
+// counts[0] += vectors on the fast path, counts[1] += results that differ.
+__device__ __forceinline__ double vn_comp(uint32_t hi, uint32_t lo)
+{
+    const unsigned long long m = ((unsigned long long)hi << 21) ^ (unsigned long long)(lo >> 11);
+    const double u = (double)(m & ((1ull << 53) - 1)) * 0x1p-53;             // [0, 1)
+    return (hi & 0x80000000u) ? -u : u;
+}
+__global__ __launch_bounds__(256) void verify_normalize_kernel(unsigned long long seed, unsigned long long i0,
+                                                               unsigned long long n, unsigned long long* counts)
+{
+    const unsigned long long i = i0 + (unsigned long long)blockIdx.x * 256 + threadIdx.x;
+    bool fp = false, bad = false;
+    if (i < i0 + n) {
+        const Philox p = philox4x32_10<false>((uint32_t)i, (uint32_t)(i >> 32), 0x6e6f726du, 0u, (uint32_t)seed,
+                                              (uint32_t)(seed >> 32));
+        const Philox q = philox4x32_10<false>((uint32_t)i, (uint32_t)(i >> 32), 0x6e6f726du, 1u, (uint32_t)seed,
+                                              (uint32_t)(seed >> 32));
+        V3 a = v3(vn_comp(p.w0, p.w1), vn_comp(p.w2, p.w3), vn_comp(q.w0, q.w1));
+        const uint32_t cls = q.w2 & 3u;
+        if (cls == 1u) {                                   // n + dir: unit normal plus a unit vector
+            const V3 nn = divs(a, sqrt(dot(a, a)));
+            a = nn + v3(vn_comp(q.w3, p.w0), vn_comp(p.w1 ^ q.w3, p.w2), vn_comp(p.w3, q.w0 ^ p.w1));
+        } else if (cls == 2u) {                            // one scale for the vector
+            const int e = (int)(q.w3 % 800u) - 400;
+            a = v3(ldexp(a.x, e), ldexp(a.y, e), ldexp(a.z, e));
+        } else if (cls == 3u) {                            // a scale per component
+            a = v3(ldexp(a.x, (int)(q.w3 % 900u) - 450), ldexp(a.y, (int)((q.w3 >> 10) % 900u) - 450),
+                   ldexp(a.z, (int)((q.w3 >> 20) % 900u) - 450));
+        }
+        const double n2 = dot(a, a);
+        const double mn = fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
+        fp = n2 >= 0x1p-760 && n2 <= 0x1p760 && mn >= 0x1p-900;
+        const V3 got = normalize(a);
+        const V3 want = divs(a, sqrt(n2));
+        bad = __double_as_longlong(got.x) != __double_as_longlong(want.x) ||
+              __double_as_longlong(got.y) != __double_as_longlong(want.y) ||
+              __double_as_longlong(got.z) != __double_as_longlong(want.z);
+        bad = bad && !(got.x != got.x && want.x != want.x);   // NaN == NaN
+    }
+    const unsigned long long nf = __popcll(__ballot(fp)), nb = __popcll(__ballot(bad));
+    if ((threadIdx.x & 63) == 0) {
+        if (nf) atomicAdd(counts, nf);
+        if (nb) atomicAdd(counts + 1, nb);
+    }
+}
+
+int launch_verify_normalize(unsigned long long seed, unsigned long long n, unsigned long long* d_counts)
+{
+    const unsigned long long per = 1ull << 30;          // launches of at most 2^30 vectors
+    for (unsigned long long i0 = 0; i0 < n; i0 += per) {
+        const unsigned long long m = std::min(per, n - i0);
+        hipLaunchKernelGGL(verify_normalize_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, nullptr, seed,
+                           i0, m, d_counts);
+    }
+    return hipGetLastError();
 }
 
 int launch_verify_spheres(const KParams& kp, const double* d_rays, long long n, unsigned long long* d_counts)

@@ -61,6 +61,8 @@ def lib():
         L.rt_selftest_math.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         L.rt_verify_sampler_phi.argtypes = [C.c_ulonglong, C.c_ulonglong, C.c_void_p]
         L.rt_verify_sphere_pass.argtypes = [P(Scene), C.c_void_p, C.c_longlong, C.c_void_p]
+        if hasattr(L, "rt_verify_normalize"):    # (older builds in A/B runs lack the diagnostic)
+            L.rt_verify_normalize.argtypes = [C.c_ulonglong, C.c_ulonglong, C.c_void_p]
         L.rt_accumulate_async.argtypes = [C.c_void_p, P(Params), C.c_longlong, P(Tiling), C.c_void_p, C.c_void_p]
         L.rt_resolve_async.argtypes = [C.c_void_p, P(Params), C.c_int, P(Tiling), P(Frame), C.c_void_p]
         L.rt_set_denoise_hook.argtypes = [DENOISE_FN]
@@ -82,7 +84,7 @@ EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error",
                     "rt_scene_release", "rt_render_async", "rt_assemble_async", "rt_count_async",
                     "rt_selftest_math", "rt_accumulate_async", "rt_resolve_async", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
                     "rt_denoise_unpack", "rt_denoise_pack_async", "rt_verify_sampler_phi",
-                    "rt_verify_sphere_pass", "rt_set_zero_throughput_exit", "rt_set_fill_spp_chunks",
+                    "rt_verify_sphere_pass", "rt_verify_normalize", "rt_set_zero_throughput_exit", "rt_set_fill_spp_chunks",
                     "rt_scene_cache_clear"]
 
 # rt_denoise_fn (rt.h): denoiser()'s signature, denoiser.h:31
@@ -281,6 +283,14 @@ def verify_sampler_phi(r0=0, n=1 << 31):
     """(fallbacks, mismatches) of the fast phi path over rand() values [r0, r0 + n)."""
     out = (C.c_ulonglong * 2)()
     check(lib().rt_verify_sampler_phi(r0, n, out))
+    return int(out[0]), int(out[1])
+
+
+def verify_normalize(seed=1, n=1 << 30):
+    """(fast-path vectors, mismatches) of the kernel's normalize against IEEE
+    a / sqrt(a.a) on n pseudo-random vectors (rt_verify_normalize)."""
+    out = (C.c_ulonglong * 2)()
+    check(lib().rt_verify_normalize(seed, n, out))
     return int(out[0]), int(out[1])
 
 
