@@ -140,6 +140,7 @@ struct rt_device_scene {
     DevMat* tri_mat = nullptr;       // rt_triangle.mat per triangle (RT_SEM_CUDA)
     double cbb[6] = {0, 0, 0, 0, 0, 0};   // triangles' box (RT_SEM_CUDA hit_BBox)
     double* sph_rinv = nullptr;      // 1/radius per sphere
+    double* sph_disp = nullptr;      // hsl round trip of each sphere's emission
     int sky_w = 0, sky_h = 0;
     int* tri_orig = nullptr;         // leaf order -> caller's triangle index
     int bvh_nodes = 0, bvh_depth = 0;
@@ -160,6 +161,49 @@ bool shading_bounded(const DevMat& m)
     for (double x : v)
         if (!(std::fabs(x) <= 0x1p100)) return false;
     return true;
+}
+
+// rgb_to_hsl then hsl_to_rgb (rtutility.h:81-165, main.c:155-158): the colour
+// tracer adds when a primary ray sees an emitter.  It depends on the
+// emission alone, so each sphere's is computed here once, with the same IEEE
+// operations in the same order as the kernel's hsl_roundtrip (which still
+// serves triangles and the sky sphere, whose material depends on the hit).
+double hue_to_rgb_host(double t1, double t2, double hue)
+{
+    if (hue < 0.0) hue += 1.0;
+    if (hue > 1.0) hue -= 1.0;
+    if (6.0 * hue < 1.0) return t1 + (t2 - t1) * 6.0 * hue;
+    if (2.0 * hue < 1.0) return t2;
+    if (3.0 * hue < 2.0) return t1 + (t2 - t1) * (2.0 / 3.0 - hue) * 6.0;
+    return t1;
+}
+void hsl_roundtrip_host(const rt_vec3& rgb, double out[3])
+{
+    const double r = rgb.e[0], g = rgb.e[1], b = rgb.e[2];
+    const double mx = (r > g) ? ((r > b) ? r : b) : ((g > b) ? g : b);
+    const double mn = (r < g) ? ((r < b) ? r : b) : ((g < b) ? g : b);
+    double h = 0.0, sat, l = (mx + mn) / 2.0;
+    if (mx == mn) {
+        h = 0.0;
+        sat = 0.0;
+    } else {
+        const double d = mx - mn;
+        sat = (l < 0.5) ? (d / (mx + mn)) : (d / (2.0 - mx - mn));
+        if (mx == r) h = (g - b) / d + ((g < b) ? 6.0 : 0.0);
+        else if (mx == g) h = (b - r) / d + 2.0;
+        else if (mx == b) h = (r - g) / d + 4.0;
+        h /= 6.0;
+    }
+    if (sat == 0.0) {
+        out[0] = out[1] = out[2] = l;
+        return;
+    }
+    const double t2 = (l < 0.5) ? (l * (1.0 + sat)) : (l + sat - l * sat);
+    const double t1 = 2.0 * l - t2;
+    const double third = 1.0 / 3.0;
+    out[0] = hue_to_rgb_host(t1, t2, h + third);
+    out[1] = hue_to_rgb_host(t1, t2, h);
+    out[2] = hue_to_rgb_host(t1, t2, h - third);
 }
 
 DevMat to_dev(const rt_material& m)
@@ -183,6 +227,7 @@ void free_scene(rt_device_scene* s)
     (void)hipFree(s->sky);
     (void)hipFree(s->tri_mat);
     (void)hipFree(s->sph_rinv);
+    (void)hipFree(s->sph_disp);
     (void)hipFree(s->tri_orig);
     delete s;
 }
@@ -219,6 +264,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.texels = sc->texels;
     kp.tri_orig = sc->tri_orig;
     kp.sph_rinv = sc->sph_rinv;
+    kp.sph_disp = sc->sph_disp;
     kp.tri_mat = sc->tri_mat;
     kp.cuda = p->semantics == RT_SEM_CUDA ? 1 : 0;
     for (int i = 0; i < 6; ++i) kp.cbb[i] = sc->cbb[i];
@@ -548,6 +594,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     std::vector<SphCand> cand((size_t)ns_pad, SphCand{0.0, 0.0, 0.0, HUGE_VAL});
     std::vector<DevMat> sph_mat((size_t)scene->nbSpheres);
     std::vector<double> sph_rinv((size_t)scene->nbSpheres);
+    std::vector<double> sph_disp((size_t)scene->nbSpheres * 3);
     // Candidate-pass bound L >= |C_k| + R_k for every sphere (rounded up, at
     // least 2^-20); a non-finite sphere makes it +inf, which turns the
     // candidate pass into the exact scan (rt_kernels.hip spheres_closest).
@@ -563,6 +610,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         lmax = std::isfinite((double)L) && !std::isnan((double)cand[i].k) ? std::max(lmax, L) : (long double)HUGE_VAL;
         sph_mat[i] = to_dev(s.mat);
         sph_rinv[i] = 1 / s.radius;                    // divide(v, t) = v * (1/t), vec3.h:105-107
+        hsl_roundtrip_host(s.mat.emissionColor, &sph_disp[3 * (size_t)i]);
     }
     const double cand_lmax = std::isfinite((double)lmax) ? std::nextafter((double)lmax, HUGE_VAL) : HUGE_VAL;
     std::vector<DevMat> sky;
@@ -700,7 +748,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_cand, cand)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
         (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels)) ||
         (rc = upload(&ds->bvh, bvh.nodes4)) || (rc = upload(&ds->tri_orig, bvh.order)) ||
-        (rc = upload(&ds->sky, sky)) || (rc = upload(&ds->sph_rinv, sph_rinv)) ||
+        (rc = upload(&ds->sky, sky)) || (rc = upload(&ds->sph_rinv, sph_rinv)) || (rc = upload(&ds->sph_disp, sph_disp)) ||
         (rc = upload(&ds->tri_mat, tri_mat))) {
         free_scene(ds);
         return rc;

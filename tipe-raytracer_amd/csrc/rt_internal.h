@@ -16,6 +16,8 @@
 //                          tri_orig maps back to the caller's order
 //   DevMat  [nm*th*tw]     texel table (reference `material` records)
 //   DevMat  [nt]           rt_triangle.mat per triangle (RT_SEM_CUDA materials)
+//   double  [ns][3]        the colour an emitting sphere shows when seen
+//                          directly: hsl_to_rgb(rgb_to_hsl(emission))
 // Per launch: a 18-double uniform block (camera, focus, aperture, AO, W-1,
 // H-1) read through the scalar unit where used, and, when the samples of a
 // pixel are split over P chunks, a [P][pixels][9] partial-sum scratch.
@@ -80,6 +82,7 @@ struct KParams {
     int cuda;                // rt.h RT_SEM_CUDA (render_kernel_cuda)
     double cbb[6];           // RT_SEM_CUDA: the triangles' box (lo xyz, hi xyz), hit_BBox
     const double* sph_rinv;  // 1/radius per sphere (sphere_uvmapping's divide)
+    const double* sph_disp;  // per sphere: hsl round trip of its emission (main.c:155-158), 3 doubles
     int sky_w, sky_h;
     double bvh_srel, bvh_sabs;   // distance-cull slack (rt_bvh.cpp)
     float bvh_rbox;              // >= |every bound| of the tree's boxes (single-precision slab margin)

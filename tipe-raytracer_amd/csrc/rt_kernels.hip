@@ -1981,7 +1981,13 @@ struct QPath {
             bool lit = false;
             if (chain) {
                 if (mat.es > 0) {                        // direct view of a light, main.c:154-160
-                    const V3 col = hsl_roundtrip(mat.emis);
+                    V3 col;
+                    if (kind == HIT_SPHERE && !(SKY && win == kp.ns - 1)) {
+                        const double* sd = kp_here()->sph_disp + 3 * win;   // (host: the same round trip)
+                        col = v3(sd[0], sd[1], sd[2]);
+                    } else {
+                        col = hsl_roundtrip(mat.emis);
+                    }
                     acc_add(acc, ACC_RAD, col);
                     acc_add(acc, ACC_ALB, col);
                     acc_add(acc, ACC_NRM, hn);
