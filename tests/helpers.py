@@ -57,6 +57,12 @@ def sky_scene(w=16, h=8, seed=3):
     return SceneBundle(sph, None, sky=(tex, w, h))
 
 
+def sky_tree_scene():
+    """The sky scene's spheres and texels with the C4 tree mesh (BVH + sky)."""
+    sk = sky_scene()
+    return SceneBundle(sk.spheres, scenes.moved(scenes.load_tree_fixture(), scenes.TREE_MOVE), sky=sk.sky)
+
+
 def tree_scene(move=scenes.TREE_MOVE):
     """C4: README spheres + 1tree_tri.obj (1320 tris, Kd-flat materials)."""
     return SceneBundle(scenes.cornell_spheres(), scenes.moved(scenes.load_tree_fixture(), move))

@@ -342,6 +342,26 @@ def test_bvh_tie_break_on_duplicate_triangles():
     check_parity(bundle, helpers.params(24, 18, 2, 6, accel=1))
 
 
+@pytest.mark.parametrize("case", ["tree_ao", "tree", "duplicates", "grazing", "sweep", "sky_tree"])
+def test_bvh_task_queue_kernel_bitexact(case):
+    """spp_chunks > 1 with a BVH runs render_kernel_q<.., BVH>: the sphere
+    pass, then at most RT_QB_STEPS node visits per lane and round, the walk
+    resuming next round while the lane's other work waits.  Exact ties
+    (duplicate triangles), grazing rays over a fine grid (deep stacks), AO
+    casts and the sky sphere through it, bit-exact vs the oracle."""
+    bundle, p = {
+        "tree_ao": lambda: (helpers.tree_scene(), helpers.params(40, 30, 8, 8, use_ao=True, chunks=4)),
+        "tree": lambda: (helpers.tree_scene(), helpers.params(40, 30, 6, 6, chunks=3)),
+        "duplicates": lambda: (duplicate_mesh_scene(), helpers.params(40, 30, 6, 6, chunks=3)),
+        "grazing": lambda: (grazing_grid_scene(), helpers.params(40, 30, 4, 6, chunks=2)),
+        "sweep": lambda: (helpers.SceneBundle(*tipe_rt.scenes.synthetic_cornell(10, 100)),
+                          helpers.params(48, 36, 8, 6, chunks=4)),
+        "sky_tree": lambda: (helpers.sky_tree_scene(), helpers.params(32, 24, 6, 5, sky_mode=1, use_ao=True,
+                                                                       chunks=3)),
+    }[case]()
+    check_parity(bundle, p)
+
+
 def grazing_grid_scene(n=40, seed=11):
     """A fine n x n quad grid (2 n^2 triangles) just above the README box's
     floor, with a small random height on every vertex, seen from a low

@@ -74,9 +74,28 @@ def test_bvh_kernel_c4_band():
         assert_same(got[k], ref[name][400:464], name)
 
 
+def test_bvh_queue_kernel_c4_band():
+    """C4 (tree, AO 2.5 -> 2, 8 bounces) on a full-width 64-row band with
+    spp_chunks 4: the BVH task-queue kernel (resumable walks) at frame width."""
+    bundle = helpers.tree_scene()
+    p = helpers.params(1200, 900, 4, 8, use_ao=True, chunks=4)
+    ref = helpers.oracle_render(bundle, p, row_hi=463, row_lo=400, nthreads=ORACLE_THREADS)
+    import torch
+    rows = 64
+    bufs = [torch.full((rows, 1200, 3), -1.0, dtype=torch.float64, device="cuda:0") for _ in range(4)]
+    ds = tipe_rt.DeviceScene(bundle.scene, 0)
+    tipe_rt.render_async(ds, p, tipe_rt.band_tiling(400, 463), *[b.data_ptr() for b in bufs],
+                         torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ds.close()
+    got = [b.cpu().numpy() for b in bufs]
+    for k, name in enumerate(("canva", "albedo", "normal", "radiance")):
+        assert_same(got[k], ref[name][400:464], name)
+
+
 # ---- many tasks per lane: the queue kernel on a few blocks -------------------
 @pytest.mark.parametrize("blocks,case", [(1, "cornell"), (3, "cornell"), (2, "cornell_ao"), (1, "pyramid"),
-                                         (5, "aperture")])
+                                         (5, "aperture"), (2, "tree_ao"), (1, "sweep")])
 def test_queue_kernel_tiny_grid(blocks, case, monkeypatch):
     """RT_QUEUE_BLOCKS (read on every launch) shrinks the persistent grid to
     a few blocks: every lane runs hundreds of tasks, so batch re-grabs, the
@@ -90,6 +109,9 @@ def test_queue_kernel_tiny_grid(blocks, case, monkeypatch):
         "pyramid": lambda: (helpers.pyramid_scene(), helpers.params(64, 48, 12, 6, chunks=6)),
         "aperture": lambda: (helpers.cornell(), helpers.params(40, 30, 12, 5, aperture=(0.3, 0.2), compat=0,
                                                               focus=2.5, chunks=3)),
+        "tree_ao": lambda: (helpers.tree_scene(), helpers.params(40, 30, 8, 8, use_ao=True, chunks=4)),
+        "sweep": lambda: (helpers.SceneBundle(*tipe_rt.scenes.synthetic_cornell(10, 100)),
+                          helpers.params(64, 48, 12, 6, chunks=6)),
     }[case]()
     check_parity(bundle, p)
 

@@ -328,6 +328,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
         kp.bvh_srel = sc->s_rel;
         kp.bvh_sabs = sc->s_abs;
         kp.bvh_rbox = sc->bvh_rbox;
+        kp.bvh_stack = 3 * sc->bvh_depth + 1;
     }
     return RT_OK;
 }

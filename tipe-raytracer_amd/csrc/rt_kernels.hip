@@ -97,6 +97,9 @@ static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) m
 #define RT_QSTATS 0
 #endif
 #define RT_TRACE_WORDS (RT_QSTATS ? 18 : 4)
+#ifndef RT_QB_STEPS                 // queue kernel, BVH scenes: node visits per lane and round
+#define RT_QB_STEPS 3
+#endif
 #ifndef RT_NRM_RSQ                  // normalize: 1/|a| refined from the sqrt sequence's own rsq (no v_rcp_f64)
 #define RT_NRM_RSQ 1
 #endif
@@ -486,6 +489,15 @@ __device__ __forceinline__ unsigned short* bvh_stack()
 {
     __shared__ unsigned short stk_lds[kStack4 * 256];
     return stk_lds + threadIdx.x;
+}
+// The queue kernel's per-lane stack (BVH scenes): [kStackQ][256] uint16, 12 KiB,
+// which keeps the kernel at 4 blocks (16 waves) per CU; trees that could need
+// more entries (3 * depth4 + 1 > kStackQ) render with the fixed-grid kernel.
+constexpr int kStackQ = 24;
+__device__ __forceinline__ unsigned short* bvh_stack_q()
+{
+    __shared__ unsigned short stkq_lds[kStackQ * 256];
+    return stkq_lds + threadIdx.x;
 }
 // Conservative single-precision slab test (the culling only has to be a
 // superset of the double test on the padded boxes).  Per ray
@@ -2108,7 +2120,7 @@ struct QPath {
     }
 };
 
-template <bool SKY, int AOM>
+template <bool SKY, int AOM, bool BVH>
 __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
 {
     __shared__ double acc_lds[ACC_INC * 256];
@@ -2125,6 +2137,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     L.chain = true; L.ao_cast = false; L.refr = false; L.hole = false;
     L.state = SM_CAM;                // s = 0 >= s1 = 0: takes a task first
     int x = 0, g = 0, s1 = 0;
+    int node = 0, sp = 0, win_orig = 0;      // BVH walk in flight (state SM_TRAV)
     unsigned chunk = 0, p = 0, pixel = 0;
     bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
     Stream st;                       // draw stream of the sample in flight (next31 for refraction / AO)
@@ -2153,7 +2166,35 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
         qs[1] += (unsigned long long)__popcll(__ballot(L.state == SM_CAST));
 #endif
         // ---- 1. closest hit (main.c:52-92) for every lane with a ray ------
-        if (L.state == SM_CAST) {
+        if (BVH) {
+            // spheres, then the triangle BVH: up to RT_QB_STEPS node visits
+            // per round; a deeper walk resumes next round (its lane skips
+            // the path work meanwhile), so a wave never waits for its
+            // deepest lane's whole walk
+            if (L.state == SM_CAST) {
+                Cnt cnt;
+                L.win = cast_spheres<false, false>(kp, L.o, L.cast_dir(), L.best, cnt);
+                L.kind = L.win >= 0 ? HIT_SPHERE : HIT_NONE;
+                win_orig = 0;
+                node = 0;
+                sp = 0;
+                L.state = SM_TRAV;
+            }
+            if (__ballot(L.state == SM_TRAV) != 0ull) {
+                const V3 dd = L.cast_dir();
+                const Ray32 r32 = ray32(L.o, dd, kp.bvh_rbox);
+                unsigned short* stk = bvh_stack_q();
+                for (int j = 0; j < RT_QB_STEPS; ++j) {
+                    if (L.state == SM_TRAV) {
+                        Cnt cnt;
+                        if (!bvh_step<false, false>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind, L.win, win_orig,
+                                                    cnt))
+                            L.state = SM_RESOLVE;
+                    }
+                    if (__ballot(L.state == SM_TRAV) == 0ull) break;
+                }
+            }
+        } else if (L.state == SM_CAST) {
             Cnt cnt;
             L.kind = closest_hit<false, false>(kp, L.o, L.cast_dir(), L.best, L.win, cnt);
             L.state = SM_RESOLVE;
@@ -2555,29 +2596,35 @@ static void launch_variant(const KParams& kp_in, void* stream)
 }
 
 #if RT_QUEUE > 0
-template <bool SKY, int AOM>
+template <bool SKY, int AOM, bool BVH>
 static void queue_occupancy(int& nb)
 {
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<SKY, AOM>, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<SKY, AOM, BVH>, 256, 0);
 }
 
 // Resident blocks of the queue kernel on this device (grid of render_kernel_q).
 // Cached per device and variant; rt_fill_canva may run on several host
 // threads at once (main.c's pthreads), so the cache is atomic (every thread
 // computes the same value).
-static unsigned queue_grid(bool sky, bool ao)
+template <bool BVH>
+static void queue_occupancy_v(bool sky, bool ao, int& nb)
 {
-    static std::atomic<int> cached[4][64];
+    if (sky && ao) queue_occupancy<true, AO_ON, BVH>(nb);
+    else if (sky) queue_occupancy<true, AO_OFF, BVH>(nb);
+    else if (ao) queue_occupancy<false, AO_ON, BVH>(nb);
+    else queue_occupancy<false, AO_OFF, BVH>(nb);
+}
+static unsigned queue_grid(bool sky, bool ao, bool bvh)
+{
+    static std::atomic<int> cached[8][64];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0)][dev & 63];
+    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + (bvh ? 4 : 0)][dev & 63];
     int c = slot.load(std::memory_order_relaxed);
     if (c <= 0) {
         int nb = 0, ncu = 0;
-        if (sky && ao) queue_occupancy<true, AO_ON>(nb);
-        else if (sky) queue_occupancy<true, AO_OFF>(nb);
-        else if (ao) queue_occupancy<false, AO_ON>(nb);
-        else queue_occupancy<false, AO_OFF>(nb);
+        if (bvh) queue_occupancy_v<true>(sky, ao, nb);
+        else queue_occupancy_v<false>(sky, ao, nb);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         c = std::max(1, nb) * std::max(1, ncu);
         if (std::getenv("RT_QUEUE_VERBOSE")) std::fprintf(stderr, "render_kernel_q: %d blocks/CU x %d CUs -> %d\n", nb, ncu, c);
@@ -2589,6 +2636,15 @@ static unsigned queue_grid(bool sky, bool ao)
     return (unsigned)c;
 }
 
+template <bool BVH>
+static void queue_launch(bool sky, bool ao, unsigned nb, hipStream_t st, const KParams& k2)
+{
+    if (sky && ao) hipLaunchKernelGGL((render_kernel_q<true, AO_ON, BVH>), dim3(nb), dim3(256), 0, st, k2);
+    else if (sky) hipLaunchKernelGGL((render_kernel_q<true, AO_OFF, BVH>), dim3(nb), dim3(256), 0, st, k2);
+    else if (ao) hipLaunchKernelGGL((render_kernel_q<false, AO_ON, BVH>), dim3(nb), dim3(256), 0, st, k2);
+    else hipLaunchKernelGGL((render_kernel_q<false, AO_OFF, BVH>), dim3(nb), dim3(256), 0, st, k2);
+}
+
 // floor((2^32 - 1) / d) for udiv_q
 static unsigned qdiv_magic(unsigned d) { return d ? (unsigned)(0xffffffffull / d) : 0u; }
 #endif
@@ -2596,11 +2652,12 @@ static unsigned qdiv_magic(unsigned d) { return d ? (unsigned)(0xffffffffull / d
 int launch_render(const KParams& kp, void* stream)
 {
 #if RT_QUEUE > 0
-    if (kp.task_ctr && kp.chunks > 1 && !kp.bvh && !kp.cuda && !kp.sums) {
+    const bool qbvh = kp.bvh != nullptr && RT_QB_STEPS > 0 && kp.bvh_stack <= kStackQ;
+    if (kp.task_ctr && kp.chunks > 1 && (!kp.bvh || qbvh) && !kp.cuda && !kp.sums) {
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
-        const unsigned nb = queue_grid(sky, ao);
+        const unsigned nb = queue_grid(sky, ao, qbvh);
         unsigned long long* tr = nullptr;
         const char* tf = std::getenv("RT_QUEUE_TRACE");
         if (tf) (void)hipMalloc((void**)&tr, (size_t)nb * 256 * RT_TRACE_WORDS * sizeof(unsigned long long));
@@ -2614,10 +2671,8 @@ int launch_render(const KParams& kp, void* stream)
         // chunk starts c*S/P in 32 bits when (P + 1) * S fits
         k2.qm_chunks = (unsigned long long)(kp.chunks + 1) * (unsigned long long)kp.S < (1ull << 32)
                            ? qdiv_magic((unsigned)kp.chunks) : 0u;
-        if (sky && ao) hipLaunchKernelGGL((render_kernel_q<true, AO_ON>), dim3(nb), dim3(256), 0, st, k2);
-        else if (sky) hipLaunchKernelGGL((render_kernel_q<true, AO_OFF>), dim3(nb), dim3(256), 0, st, k2);
-        else if (ao) hipLaunchKernelGGL((render_kernel_q<false, AO_ON>), dim3(nb), dim3(256), 0, st, k2);
-        else hipLaunchKernelGGL((render_kernel_q<false, AO_OFF>), dim3(nb), dim3(256), 0, st, k2);
+        if (qbvh) queue_launch<true>(sky, ao, nb, st, k2);
+        else queue_launch<false>(sky, ao, nb, st, k2);
         if (tr) {
             std::vector<unsigned long long> h((size_t)nb * 256 * RT_TRACE_WORDS);
             (void)hipStreamSynchronize(st);

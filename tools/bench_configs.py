@@ -32,6 +32,8 @@ CONFIGS = {
     "C4": (scenes.tree_mesh, 16, 8, True, 2.5, 2000, 1200, 900, 4),
     # C5: 4K frame of the C3 scene (SURVEY.md §8 config resolution), 5000 spp over 8 GPUs
     "C5": (scenes.pyramid_mesh, 20, 6, False, 2.5, 5000, 3840, 2880, 8),
+    # roofline-sweep scene: README box + 10 random spheres... (synthetic_cornell(10, 100))
+    "SWEEP": ("sweep", 32, 6, False, 2.5, 32, 1200, 900, 1),
 }
 
 
@@ -39,7 +41,11 @@ def run(name, spp_scale, dev, stream):
     mesh_fn, spp, bounces, ao, ao_int, full_spp, W, H, gpus = CONFIGS[name]
     spp = max(1, int(spp * spp_scale))
     spheres = scenes.cornell_spheres()
-    if mesh_fn is None:
+    if mesh_fn == "sweep":
+        spheres, (tris, qm, mats, tw, th, nm) = scenes.synthetic_cornell(10, 100)
+        scene = tipe_rt.make_scene(spheres, tris, qm, mats, tw, th, nm)
+        nt = len(tris)
+    elif mesh_fn is None:
         scene = tipe_rt.make_scene(spheres)
         nt = 0
     else:
