@@ -328,7 +328,8 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
         kp.bvh_srel = sc->s_rel;
         kp.bvh_sabs = sc->s_abs;
         kp.bvh_rbox = sc->bvh_rbox;
-        kp.bvh_stack = 3 * sc->bvh_depth + 1;
+        // the queue kernel's uint16 stack entries: node index, or 0x8000 | triangle
+        kp.bvh_stack = (sc->bvh_nodes < 0x8000 && sc->nt <= 0x8000) ? 3 * sc->bvh_depth + 1 : 1 << 30;
     }
     return RT_OK;
 }

@@ -573,6 +573,17 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
     bool h[4];
     float tn[4];
     box4(kp, nd, r32, cull32(kp, best), h, tn);
+#ifdef RT_DUP_BOX
+    {
+        bool h2[4];
+        float tn2[4];
+        Ray32 q = r32;
+        q.ax = launder(q.ax);
+        box4(kp, nd, q, cull32(kp, best), h2, tn2);
+        if (opaque_false())
+            for (int c = 0; c < 4; ++c) { h[c] = h2[c]; tn[c] = tn2[c]; }
+    }
+#endif
     int next = -1;
     float tnext = 0.0f;
     unsigned lm = 0;                                     // hit leaf slots
@@ -2180,11 +2191,17 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 sp = 0;
                 L.state = SM_TRAV;
             }
+            QT(13)
             if (__ballot(L.state == SM_TRAV) != 0ull) {
                 const V3 dd = L.cast_dir();
                 const Ray32 r32 = ray32(L.o, dd, kp.bvh_rbox);
                 unsigned short* stk = bvh_stack_q();
+#pragma unroll 1
                 for (int j = 0; j < RT_QB_STEPS; ++j) {
+#if RT_QSTATS
+                    qs[6] += 1;
+                    qs[7] += (unsigned long long)__popcll(__ballot(L.state == SM_TRAV));
+#endif
                     if (L.state == SM_TRAV) {
                         Cnt cnt;
                         if (!bvh_step<false, false>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind, L.win, win_orig,
