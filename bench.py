@@ -471,8 +471,10 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(scene, cam, threads=args.cpu_threads)
             rec["speedup_vs_cpu_baseline"] = round(value / rec["cpu_baseline"]["value"], 1)
-        print(json.dumps(rec))
+        print(json.dumps(rec), flush=True)
     ds.close()
+    torch.cuda.synchronize(dev)
+    tipe_rt.lib().rt_shutdown()      # cached scenes, pooled streams and pinned buffers of the drop-in legs
     if world > 1:
         dist.destroy_process_group()
 

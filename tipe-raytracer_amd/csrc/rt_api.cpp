@@ -299,6 +299,11 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     uni[U_FOCUS] = focus;
     uni[U_OX] = ox;
     uni[U_OY] = oy;
+    // camera.h:49-54: the ray starts at origin + (jx*ox, jy*oy, 0); with ox = oy = 0
+    // the offsets are +-0 and the sum is the origin itself unless a coordinate is -0
+    kp.cam_pin = ox == 0.0 && oy == 0.0 && !(p->cam.origin.e[0] == 0.0 && std::signbit(p->cam.origin.e[0])) &&
+                 !(p->cam.origin.e[1] == 0.0 && std::signbit(p->cam.origin.e[1])) &&
+                 !(p->cam.origin.e[2] == 0.0 && std::signbit(p->cam.origin.e[2]));
     uni[U_AO] = AO;
     uni[U_WM1] = (double)(p->largeur_image - 1);    // main.c:265 (largeur_image-1)
     uni[U_HM1] = (double)(p->hauteur_image - 1);
@@ -425,7 +430,7 @@ struct PooledStream {
 };
 
 std::mutex g_pool_mu;
-std::vector<PooledStream*> g_pool_free;    // idle streams (any device); never destroyed
+std::vector<PooledStream*> g_pool_free;    // idle streams (any device); destroyed by rt_shutdown
 
 int stream_pool_get(int device, PooledStream** out)
 {
@@ -454,6 +459,25 @@ void stream_pool_put(PooledStream* ps)
 {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     g_pool_free.push_back(ps);
+}
+
+// Idle pooled streams and their pinned staging buffers (streams a call still
+// holds go back to the pool when it returns and are released by the next
+// rt_shutdown).
+void stream_pool_clear()
+{
+    std::vector<PooledStream*> idle;
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        idle.swap(g_pool_free);
+    }
+    for (PooledStream* ps : idle) {
+        DeviceGuard g(ps->device);
+        (void)hipStreamSynchronize(ps->st);
+        (void)hipStreamDestroy(ps->st);
+        if (ps->host) (void)hipHostFree(ps->host);
+        delete ps;
+    }
 }
 
 // Exact bytes of everything rt_scene_upload reads.
@@ -564,6 +588,7 @@ void rt_shutdown(void)
         g_inited = false;
     }
     scene_cache_clear();
+    stream_pool_clear();
 }
 
 const char* rt_last_error(void) { return g_err.c_str(); }

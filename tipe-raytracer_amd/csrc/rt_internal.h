@@ -94,6 +94,7 @@ struct KParams {
     int W, H, S, B;
     int useAO;
     int zero_exit;           // paths end once rayColor == 0 (host: only where exact, LanePath::zero_rc)
+    int cam_pin;             // aperture 0 and no -0 camera coordinate: co + (jx*0, jy*0, 0) == co exactly
     uint32_t key0, key1;
     int chunks;              // samples of a pixel split into this many chunks
     // tiling

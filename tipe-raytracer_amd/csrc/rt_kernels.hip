@@ -2327,22 +2327,26 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 CamDraws w{blk, 0};
                 const double ju = -0.5 + 1.0 * unit31(w.next31());     // randomDouble(-0.5, 0.5)
                 const double jv = -0.5 + 1.0 * unit31(w.next31());
-                const double jx = -0.5 + 1.0 * unit31(w.next31());
-                const double jy = -0.5 + 1.0 * unit31(w.next31());
                 const int b = opq0();
                 const cdptr U = (cdptr)kp.uni;
                 const double nu = (double)x + ju, nv = (double)g + jv;
                 const double rcw = U[b + U_RC_WM1], rch = U[b + U_RC_HM1];
                 const double u = rcw != 0.0 ? div_core(nu, U[b + U_WM1], rcw) : nu / U[b + U_WM1];
                 const double v = rch != 0.0 ? div_core(nv, U[b + U_HM1], rch) : nv / U[b + U_HM1];
-                const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
                 const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
                 const V3 ch = v3(U[b + U_CAM_H], U[b + U_CAM_H + 1], U[b + U_CAM_H + 2]);
                 const V3 cv = v3(U[b + U_CAM_V], U[b + U_CAM_V + 1], U[b + U_CAM_V + 2]);
                 const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
                 const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));     // get_ray, camera.h:42-55
                 const V3 dest = co + muls(dir, U[b + U_FOCUS]);
-                no = co + v3(dx, dy, 0);
+                if (kp.cam_pin) {                              // zero aperture: the origin itself (host-checked)
+                    no = co;
+                } else {
+                    const double jx = -0.5 + 1.0 * unit31(w.next31());
+                    const double jy = -0.5 + 1.0 * unit31(w.next31());
+                    const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
+                    no = co + v3(dx, dy, 0);
+                }
                 X = dest - no;
             } else {
                 // random_dir_no_norm (rtutility.h:189-203), then n + dir (main.c:163)
