@@ -2,8 +2,8 @@
 // (the reference scans every triangle, main.c:80-90, and
 // its CUDA path only has a per-mesh slab box, triangle.hu:42-59).
 //
-// Binary BVH, binned SAH (16 bins on the widest centroid axis), leaves of at
-// most 4 triangles (more only at the depth cap).  Each node stores the boxes
+// Binary BVH, binned SAH (16 bins on the widest centroid axis), one triangle
+// per leaf (kLeaf; more only at the depth cap or for identical centroids).  Each node stores the boxes
 // of BOTH children (float, rounded outward), so one 64-byte node fetch
 // decides both descents.  Node 0
 // is the root split; triangles are reordered into leaf order and the kernel
@@ -72,7 +72,7 @@ struct Ref {
     Box box;
 };
 
-int kLeaf = 2;                // leaf size target (RT_BVH_LEAF overrides, for tuning; 1-2 measured best)
+int kLeaf = 1;                // leaf size target (RT_BVH_LEAF overrides, for tuning; 1 measured best with the queue kernel)
 
 // Outward rounding of a double bound to float.
 float down(double x)
