@@ -502,17 +502,20 @@ __device__ __forceinline__ unsigned short* bvh_stack_q()
 // Conservative single-precision slab test (the culling only has to be a
 // superset of the double test on the padded boxes).  Per ray
 // and axis: inv = rcp((float)d) (|d| clamped to >= 2^-60; <= 2 ulp of 1/d),
-// and two offsets a, b = -(float)o * inv -/+ s E with s = sign(inv) and
+// and the offsets a = -(float)o * inv - E, b = -(float)o * inv + E with
 //   E = 2^-19 (rbox + |(float)o|) |inv|,
-// rbox >= every |bound| of the tree.  The near and far slab distances
-// fma(lo, inv, a) and fma(hi, inv, b) then lie below / above the exact
-// (bound - o) / d: the rounding of d, o, inv, o*inv, the offsets and the fma
-// together stay within 6 u (rbox + |o|) |inv| + 2 u E < E / 5 (u = 2^-24).
+// rbox >= every |bound| of the tree.  The entry plane of an axis is the lo
+// bound when inv >= 0 and the hi bound when inv < 0 (the other is the exit
+// plane), so with P the entry and Q the exit bound, fma(P, inv, a) and
+// fma(Q, inv, b) lie below / above the exact (P - o) / d and (Q - o) / d:
+// the rounding of d, o, inv, o*inv, the offsets and the fma together stay
+// within 6 u (rbox + |o|) |inv| + 2 u E < E / 5 (u = 2^-24).  (These are the
+// min and max of the two plane distances: lo <= hi and a < b order them.)
 // The cull thresholds are rounded outward in the same way.
 struct Ray32 {
     float ix, iy, iz;            // ~1/d
-    float ax, ay, az;            // offsets of the lo bounds
-    float bx, by, bz;            // offsets of the hi bounds
+    float ax, ay, az;            // offsets of the entry planes (lower bounds)
+    float bx, by, bz;            // offsets of the exit planes (upper bounds)
 };
 __device__ __forceinline__ void ray32_axis(double oc, double dc, float rbox, float& inv, float& a, float& b)
 {
@@ -522,9 +525,8 @@ __device__ __forceinline__ void ray32_axis(double oc, double dc, float rbox, flo
     const float of = (float)oc;
     const float oi = of * inv;
     const float E = 0x1p-19f * ((rbox + fabsf(of)) * fabsf(inv));
-    const float sE = inv >= 0.0f ? E : -E;
-    a = -oi - sE;
-    b = -oi + sE;
+    a = -oi - E;
+    b = -oi + E;
 }
 __device__ __forceinline__ Ray32 ray32(const V3 o, const V3 d, float rbox)
 {
@@ -539,18 +541,24 @@ __device__ __forceinline__ float cull32(const KParams& kp, double best)
 {
     return (float)fma(best, 1.0 + kp.bvh_srel, kp.bvh_sabs) * (1.0f + 0x1p-22f);
 }
-// The four child boxes of a node: hit flags and near distances.
+// The four child boxes of a node: hit flags and near distances.  The entry
+// and exit planes of each axis are picked by the sign of inv (one 16-byte
+// row of lo or hi per axis: BvhNode4 stores lo[3][4] then hi[3][4]).
 __device__ __forceinline__ void box4(const KParams& kp, const BvhNode4* nd, const Ray32& r, float cull, bool h[4],
                                      float tn[4])
 {
     const float nsabs = (float)(-kp.bvh_sabs) * (1.0f + 0x1p-22f);
+    const float4* rows = (const float4*)nd;             // rows 0-2: lo x/y/z, rows 3-5: hi x/y/z
+    const int sx = (int)(__float_as_uint(r.ix) >> 31) * 3, sy = (int)(__float_as_uint(r.iy) >> 31) * 3,
+              sz = (int)(__float_as_uint(r.iz) >> 31) * 3;
+    const float4 px = rows[sx], py = rows[1 + sy], pz = rows[2 + sz];
+    const float4 qx = rows[3 - sx], qy = rows[4 - sy], qz = rows[5 - sz];
+    const float Px[4] = {px.x, px.y, px.z, px.w}, Py[4] = {py.x, py.y, py.z, py.w}, Pz[4] = {pz.x, pz.y, pz.z, pz.w};
+    const float Qx[4] = {qx.x, qx.y, qx.z, qx.w}, Qy[4] = {qy.x, qy.y, qy.z, qy.w}, Qz[4] = {qz.x, qz.y, qz.z, qz.w};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const float x0 = fmaf(nd->lo[0][c], r.ix, r.ax), x1 = fmaf(nd->hi[0][c], r.ix, r.bx);
-        const float y0 = fmaf(nd->lo[1][c], r.iy, r.ay), y1 = fmaf(nd->hi[1][c], r.iy, r.by);
-        const float z0 = fmaf(nd->lo[2][c], r.iz, r.az), z1 = fmaf(nd->hi[2][c], r.iz, r.bz);
-        const float tmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1));
-        const float tmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
+        const float tmin = fmaxf(fmaxf(fmaf(Px[c], r.ix, r.ax), fmaf(Py[c], r.iy, r.ay)), fmaf(Pz[c], r.iz, r.az));
+        const float tmax = fminf(fminf(fmaf(Qx[c], r.ix, r.bx), fmaf(Qy[c], r.iy, r.by)), fmaf(Qz[c], r.iz, r.bz));
         h[c] = nd->count[c] >= 0 && tmin <= tmax && tmax >= nsabs && tmin <= cull;
         tn[c] = tmin;
     }
@@ -1932,18 +1940,27 @@ __device__ __forceinline__ int chunk_start(int S, int chunks, unsigned qm_chunks
 // (tracer multiplies rayColor by it and then returns incomingLight).
 enum : int { ROLE_NONE = 0, ROLE_BOUNCE = 1, ROLE_CAMERA = 2 };
 
+// What resolve_hit leaves for next_ray / finish_bounce in the same round (not
+// live across rounds, so not in QPath: the cast and the BVH walk do not carry
+// these registers).
+struct QHit {
+    V3 hn;                           // the hit's normal
+    double rs;                       // its reflectionStrength
+    bool refr, hole;                 // refraction decided after the direction draws; alpha hole
+};
+
 template <bool SKY, int AOM>
 struct QPath {
-    V3 o, d, cd, inc, rc, hn;        // cd: the cast's direction (AO casts; else d)
-    double top_n2, best, rs;
+    V3 o, d, cd, inc, rc;            // cd: the cast's direction (AO casts; else d)
+    double top_n2, best;
     int i, kind, win, s, state;
-    bool chain, ao_cast, refr, hole;
+    bool chain, ao_cast;
 
     __device__ __forceinline__ V3 cast_dir() const { return AOM == AO_ON ? cd : d; }
 
     // The hit's material (tri_material / sky_material are pure functions of
     // the hit, so a refraction lane recomputes it instead of keeping it live).
-    __device__ __forceinline__ Mat hit_material(const KParams& kp, V3 hp) const
+    __device__ __forceinline__ Mat hit_material(const KParams& kp, V3 hp, V3 hn) const
     {
         if (kind == HIT_SPHERE) {
             Mat mat = load_mat(kp.sph_mat + win);
@@ -1960,7 +1977,7 @@ struct QPath {
 
     // After a cast (state SM_RESOLVE).  Returns the role for next_ray, or
     // ROLE_NONE; a lane whose path is over gets state SM_CAM (sum added).
-    __device__ __forceinline__ int resolve_hit(const KParams& kp, double* acc)
+    __device__ __forceinline__ int resolve_hit(const KParams& kp, double* acc, QHit& H)
     {
         bool ended = false, add_inc = true;
         int role = ROLE_NONE;
@@ -1995,12 +2012,12 @@ struct QPath {
             const V3 hp = o + muls(d, best);             // ray_at
             if (kind == HIT_SPHERE) {
                 const SphGeo sg = kp.sph[win];
-                hn = normalize(hp - v3(sg.cx, sg.cy, sg.cz));
+                H.hn = normalize(hp - v3(sg.cx, sg.cy, sg.cz));
             } else {
                 const TriGeo tg = kp.tri[win];
-                hn = normalize(v3(tg.nx, tg.ny, tg.nz));
+                H.hn = normalize(v3(tg.nx, tg.ny, tg.nz));
             }
-            const Mat mat = hit_material(kp, hp);
+            const Mat mat = hit_material(kp, hp, H.hn);
             bool lit = false;
             if (chain) {
                 if (mat.es > 0) {                        // direct view of a light, main.c:154-160
@@ -2013,11 +2030,11 @@ struct QPath {
                     }
                     acc_add(acc, ACC_RAD, col);
                     acc_add(acc, ACC_ALB, col);
-                    acc_add(acc, ACC_NRM, hn);
+                    acc_add(acc, ACC_NRM, H.hn);
                     lit = true;
                 } else if (!(mat.alpha < 0.0001) || i == kp.B - 1) {
                     acc_add(acc, ACC_ALB, mat.diff);
-                    acc_add(acc, ACC_NRM, hn);
+                    acc_add(acc, ACC_NRM, H.hn);
                     chain = mat.alpha < 0.0001;
                 }
             }
@@ -2026,16 +2043,16 @@ struct QPath {
                 add_inc = false;
             } else {
                 o = hp;
-                rs = mat.rs;
-                refr = false;
-                hole = mat.alpha < 0.0001;
-                if (hole) {                              // alpha hole: straight on, main.c:200-206;
+                H.rs = mat.rs;
+                H.refr = false;
+                H.hole = mat.alpha < 0.0001;
+                if (H.hole) {                              // alpha H.hole: straight on, main.c:200-206;
                     if (i + 1 >= kp.B) ended = true;     // its direction draws are made (and unused)
                     else role = ROLE_BOUNCE;             // so the stream's block cache stays in order
                 } else {
                     chain = false;
                     if (mat.alpha <= 0.99) {             // refraction: decided after the direction draws
-                        refr = true;
+                        H.refr = true;
                         role = ROLE_BOUNCE;
                     } else {
                         shade(kp, mat);
@@ -2072,23 +2089,23 @@ struct QPath {
     __device__ __forceinline__ void shade(const KParams& kp, const Mat& mat) { shade_with(kp, mat.emis, mat.es, mat.diff); }
 
     // After next_ray gave a bounce lane its diffuse direction dn.
-    __device__ __forceinline__ void finish_bounce(const KParams& kp, V3 dn, Stream& st, double* acc)
+    __device__ __forceinline__ void finish_bounce(const KParams& kp, V3 dn, Stream& st, double* acc, const QHit& H)
     {
-        if (hole) {                                      // the ray goes on unchanged from the hit point
+        if (H.hole) {                                      // the ray goes on unchanged from the hit point
             ++i;
             cd = d;
             state = SM_CAST;
             return;
         }
-        const V3 reflected_dir = d - muls(hn, 2 * dot(d, hn));
-        const V3 dr = dn + muls(reflected_dir - dn, rs);
+        const V3 reflected_dir = d - muls(H.hn, 2 * dot(d, H.hn));
+        const V3 dr = dn + muls(reflected_dir - dn, H.rs);
         bool shaded = true;
-        if (refr) {                                      // main.c:167-193
-            const Mat mat = hit_material(kp, o);
-            V3 nn = hn;
+        if (H.refr) {                                      // main.c:167-193
+            const Mat mat = hit_material(kp, o, H.hn);
+            V3 nn = H.hn;
             double n1, n2;
-            if (dot(d, hn) > 0) {                        // leaving: pop restores the stack
-                nn = v3(-hn.x, -hn.y, -hn.z);
+            if (dot(d, H.hn) > 0) {                        // leaving: pop restores the stack
+                nn = v3(-H.hn.x, -H.hn.y, -H.hn.z);
                 n1 = mat.ior;
                 n2 = top_n2;
             } else {                                     // entering: push (top.n2, ior)
@@ -2109,11 +2126,11 @@ struct QPath {
             d = dr;
         }
         bool ended = false;
-        if (refr && shaded) ended = zero_rc(kp);
+        if (H.refr && shaded) ended = zero_rc(kp);
         if (AOM == AO_ON && shaded && !ended && i + 1 < kp.B) {
             // ambient_occlusion's cast (main.c:96-103): from the hit along n + random
             Cnt cnt;
-            cd = normalize(hn + random_dir<false>(st, cnt));
+            cd = normalize(H.hn + random_dir<false>(st, cnt));
             ao_cast = true;
             state = SM_CAST;
             return;
@@ -2141,11 +2158,11 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     const int lane = threadIdx.x & 63;
     unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
     QPath<SKY, AOM> L;
-    L.o = L.d = L.cd = L.inc = L.rc = L.hn = v3(0, 0, 0);
+    L.o = L.d = L.cd = L.inc = L.rc = v3(0, 0, 0);
     L.top_n2 = 1.0;
-    L.best = L.rs = 0.0;
+    L.best = 0.0;
     L.i = 0; L.kind = HIT_NONE; L.win = -1; L.s = 0;
-    L.chain = true; L.ao_cast = false; L.refr = false; L.hole = false;
+    L.chain = true; L.ao_cast = false;
     L.state = SM_CAM;                // s = 0 >= s1 = 0: takes a task first
     int x = 0, g = 0, s1 = 0;
     int node = 0, sp = 0, win_orig = 0;      // BVH walk in flight (state SM_TRAV)
@@ -2219,7 +2236,11 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
         QT(8)
         // ---- 2. the hit, up to the next direction --------------------------
         int role = ROLE_NONE;
-        if (L.state == SM_RESOLVE) role = L.resolve_hit(kp, acc);
+        QHit H;
+        H.hn = v3(0, 0, 0);
+        H.rs = 0.0;
+        H.refr = H.hole = false;
+        if (L.state == SM_RESOLVE) role = L.resolve_hit(kp, acc, H);
         QT(9)
         // ---- 3. lanes whose task is done take the next one -----------------
         const bool need = L.state == SM_CAM && L.s >= s1;
@@ -2360,7 +2381,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                     pm_sincosf((float)phi, sp_, cp_);
                 }
                 pm_sincosf((float)theta, st_, ct_);
-                X = L.hn + normalize(v3((double)(ct_ * sp_), (double)(st_ * sp_), (double)cp_));
+                X = H.hn + normalize(v3((double)(ct_ * sp_), (double)(st_ * sp_), (double)cp_));
                 st.n += 2;
             }
             const V3 dn = normalize(X);
@@ -2379,7 +2400,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 st.start(pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1, rng);
                 st.n = 4;                                      // draws 0-3 were the camera's
             } else {
-                L.finish_bounce(kp, dn, st, acc);
+                L.finish_bounce(kp, dn, st, acc, H);
             }
         }
         QT(12)
