@@ -7,9 +7,12 @@ One step = one full frame of config C2 (README 10-sphere Cornell box,
 1200x900, 1000 spp, 6 bounces; Philox stream, seed 1010) rendered into HBM.
 With N > 1 (launched one rank per GPU by torch.distributed.run) the frame is
 split into cyclic 2-row tiles (tile t -> rank t mod N), each rank renders its
-tiles, the tiles are gathered to rank 0 over RCCL (torch.distributed.gather,
-backend "nccl") and rank 0 un-permutes them (rt_assemble_async): total work
-per step is fixed, so scaling is "strong".
+tiles, the tiles' colour (the canva plane: write_color_canva integers, exact
+in float32, so 12 B/px -- SURVEY §8(e)'s float3 colour payload; `--gather
+all` sends canva + albedo + normal as doubles, 72 B/px, for a denoiser) is
+gathered to rank 0 over RCCL (torch.distributed.gather, backend "nccl") and
+rank 0 un-permutes it (rt_assemble_async): total work per step is fixed, so
+scaling is "strong".
 
 Rank 0 prints ONE JSON line.  Besides the C2 headline it carries (N = 1,
 rank 0): `configs` (C3, C4, C5 and the 10-sphere/100-triangle sweep scene at
@@ -295,6 +298,9 @@ def main():
                     help="N>1: rank 0 re-renders the frame alone and checks the assembled planes bit for bit")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="one stream: frame k+1 starts after frame k (default: two streams, see step())")
+    ap.add_argument("--gather", default="colour", choices=["colour", "all"],
+                    help="N>1 payload: colour = the canva plane as float32 (12 B/px); all = canva, albedo and "
+                         "normal as float64 (72 B/px, what a denoiser needs)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: gather through host copies (rehearsing N>1 with all ranks on one GPU); "
                          "nccl (= RCCL) is the measured configuration")
@@ -331,11 +337,17 @@ def main():
     streams = [stream] if nbuf == 1 else [torch.cuda.Stream(dev) for _ in range(nbuf)]
     # frame planes: canva | albedo | normal (the reference's three outputs)
     locals_ = [torch.empty((3, rows, W, 3), dtype=torch.float64, device=dev) for _ in range(nbuf)]
-    gathered_ = gather_lists = fulls = [None] * nbuf
+    colour = args.gather == "colour"
+    npl = 1 if colour else 3                  # planes gathered and assembled
+    gdt = torch.float32 if colour else torch.float64
+    sends = [torch.empty((npl, rows, W, 3), dtype=gdt, device=dev) for _ in range(nbuf)] if colour else locals_
+    gathered_ = gather_lists = fulls = gathered64_ = [None] * nbuf
     if world > 1 and rank == 0:
-        gathered_ = [torch.empty((world, 3, rows, W, 3), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+        gathered_ = [torch.empty((world, npl, rows, W, 3), dtype=gdt, device=dev) for _ in range(nbuf)]
         gather_lists = [[g[r] for r in range(world)] for g in gathered_]
-        fulls = [torch.empty((3, H, W, 3), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+        gathered64_ = ([torch.empty((world, npl, rows, W, 3), dtype=torch.float64, device=dev) for _ in range(nbuf)]
+                       if colour else gathered_)
+        fulls = [torch.empty((npl, H, W, 3), dtype=torch.float64, device=dev) for _ in range(nbuf)]
     last = [0]
 
     def step(k):
@@ -347,18 +359,24 @@ def main():
             tipe_rt.render_async(ds, p, tiling, local[0].data_ptr(), local[1].data_ptr(), local[2].data_ptr(),
                                  None, st.cuda_stream)
             if world > 1:
+                send = sends[b]
+                if colour:
+                    send[0].copy_(local[0])                  # canva integers, exact in float32
                 if args.dist_backend == "nccl":
-                    dist.gather(local, gather_list, dst=0)     # RCCL over xGMI
+                    dist.gather(send, gather_list, dst=0)      # RCCL over xGMI
                 else:
-                    host = [torch.empty_like(local, device="cpu") for _ in range(world)] if rank == 0 else None
-                    dist.gather(local.cpu(), host, dst=0)
+                    host = [torch.empty_like(send, device="cpu") for _ in range(world)] if rank == 0 else None
+                    dist.gather(send.cpu(), host, dst=0)
                     if rank == 0:
                         for r in range(world):
                             gathered[r].copy_(host[r])
                 if rank == 0:
-                    for pl in range(3):                     # (world, plane, rows, W, 3) -> (plane, H, W, 3)
-                        tipe_rt.assemble_async(gathered[0, pl].data_ptr(), world, TILE_ROWS, rows, W, H,
-                                               full[pl].data_ptr(), st.cuda_stream, rank_stride=3 * rows * W)
+                    g64 = gathered64_[b]
+                    if colour:
+                        g64.copy_(gathered)
+                    for pl in range(npl):                   # (world, plane, rows, W, 3) -> (plane, H, W, 3)
+                        tipe_rt.assemble_async(g64[0, pl].data_ptr(), world, TILE_ROWS, rows, W, H,
+                                               full[pl].data_ptr(), st.cuda_stream, rank_stride=npl * rows * W)
 
     for k in range(args.warmup):
         step(k)
@@ -386,7 +404,7 @@ def main():
                              ref[2].data_ptr(), None, sptr)
         torch.cuda.synchronize(dev)
         used = fulls[:min(nbuf, args.warmup + args.steps)]            # every buffer that held a frame
-        verified = all(bool(torch.equal(ref, f)) for f in used)
+        verified = all(bool(torch.equal(ref[:npl], f)) for f in used)
         if not verified:
             print("verify: assembled frame differs from the single-device frame", file=sys.stderr)
 
@@ -441,6 +459,8 @@ def main():
                        "width": W, "height": H, "spp": SPP, "bounces": BOUNCES,
                        "tile_rows": TILE_ROWS if world > 1 else H, "parallelism": "row-tiles x%d" % world, "frames_in_flight": nbuf,
                        "collective": ("rccl gather" if args.dist_backend == "nccl" else "gloo gather (host)")
+                       if world > 1 else None,
+                       "gather_payload": ("canva as float32, 12 B/px" if colour else "canva+albedo+normal as float64, 72 B/px")
                        if world > 1 else None,
                        "rng": "philox4x32-10", "spp_chunks": args.chunks,
                        "arith": "fp64, reference op order (bit-exact vs oracle)"},

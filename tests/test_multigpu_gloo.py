@@ -66,11 +66,15 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         local = torch.from_numpy(render_local_frame(rank, world))
-        gl = [torch.empty_like(local) for _ in range(world)] if rank == 0 else None
-        dist.gather(local, gl, dst=0)
+        # bench.py's payload: the canva plane as float32 (write_color_canva
+        # integers 0..255, exact), 12 B/px instead of 72
+        send = local.float()
+        exact = bool((send.double() == local).all())
+        gl = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+        dist.gather(send, gl, dst=0)
         if rank == 0:
-            full = assemble([g.numpy() for g in gl], world, local.shape[0])
-            q.put(bool((full == reference_frame()).all()))
+            full = assemble([g.double().numpy() for g in gl], world, local.shape[0])
+            q.put(exact and bool((full == reference_frame()).all()))
         dist.barrier()
     finally:
         dist.destroy_process_group()
