@@ -74,7 +74,7 @@ typedef struct rt_params {
     int spp_chunks;                    /* 0/1: each pixel sums its samples in
                                           order s = 0..S-1 (fill_canva's order).
                                           P > 1: samples are summed in P fixed
-                                          contiguous slices [c*S/P, (c+1)*S/P),
+                                          contiguous slices (rt_chunk_bound),
                                           then slice sums in slice order; a
                                           deterministic grouping (independent of
                                           GPU count) that lets one pixel's
@@ -139,6 +139,21 @@ static inline int rt_resolve_spp_chunks(int spp_chunks, int spp)
     int p = spp_chunks == RT_SPP_CHUNKS_AUTO ? RT_SPP_CHUNKS_DEFAULT : spp_chunks;
     if (p <= 1 || spp <= 1) return 1;
     return p < spp ? p : spp;
+}
+
+/* Slice c (0 <= c < P) of a pixel's S samples is [rt_chunk_bound(c),
+ * rt_chunk_bound(c + 1)).  P equal slices (c*S/P) when P < 5 or S < 8*P;
+ * otherwise P - 3 equal slices followed by three tapered ones, weights
+ * 8, ..., 8, 4, 2, 1: the task-queue kernel hands out slices in order, so
+ * the tasks still running when its queue empties are short (the frame's
+ * tail).  A pure function of (c, S, P), shared by the kernels and the
+ * oracle, so images stay independent of GPU count and tiling. */
+static inline long long rt_chunk_bound(long long c, long long S, long long P)
+{
+    if (P < 5 || S < 8 * P) return c * S / P;
+    const long long U = 8 * (P - 3) + 7;
+    const long long w = c <= P - 3 ? 8 * c : c == P - 2 ? 8 * (P - 3) + 4 : c == P - 1 ? 8 * (P - 3) + 6 : U;
+    return w * S / U;
 }
 
 /* Fills defaults: RT_RNG_PHILOX, seed 1010 (main_cuda.cu's curand seed),

@@ -730,7 +730,7 @@ static void* band_worker(void* arg)
             int pixel_index = j * W + i;
             rt_color tot[3] = {v3(0, 0, 0), v3(0, 0, 0), v3(0, 0, 0)};
             for (int ch = 0; ch < P; ++ch) {
-                const int s0 = (int)(((long long)ch * S) / P), s1 = (int)(((long long)(ch + 1) * S) / P);
+                const int s0 = (int)rt_chunk_bound(ch, S, P), s1 = (int)rt_chunk_bound(ch + 1, S, P);
                 rt_color part[3] = {v3(0, 0, 0), v3(0, 0, 0), v3(0, 0, 0)};
                 for (int x = s0; x < s1; ++x) {
                     c.pixel = (uint32_t)pixel_index;

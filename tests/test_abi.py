@@ -141,3 +141,45 @@ def test_kernel_resource_usage_builds_for_gfx950():
         assert m, txt[-2000:]
         vgprs, spills = int(m.group(1)), int(m.group(2))
         assert vgprs <= max_vgpr and spills <= max_spill, (sym, vgprs, spills)
+
+
+CHUNK_C = r"""
+#include <stdio.h>
+#include "rt/rt.h"
+int main(void) {
+  const int S[] = {1, 2, 7, 8, 39, 40, 100, 1000, 2000, 5000, 1 << 30};
+  const int P[] = {1, 2, 4, 5, 6, 8, 16, 32, 64};
+  for (unsigned i = 0; i < sizeof S / sizeof S[0]; ++i)
+    for (unsigned j = 0; j < sizeof P / sizeof P[0]; ++j) {
+      int p = rt_resolve_spp_chunks(P[j], S[i]);
+      for (int c = 0; c <= p; ++c) printf("%d %d %d %lld\n", S[i], p, c, rt_chunk_bound(c, S[i], p));
+    }
+  return 0;
+}
+"""
+
+
+def test_chunk_bounds_header_matches_mirror(tmp_path):
+    """rt.h rt_chunk_bound (compiled here) equals the Python mirror; slices
+    cover [0, S) in order, are non-empty, equal before the taper and halve
+    over the last three when tapered."""
+    src = tmp_path / "chunks.c"
+    src.write_text(CHUNK_C)
+    exe = tmp_path / "chunks"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    rows = [tuple(int(x) for x in line.split()) for line in
+            subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines()]
+    by = {}
+    for S, P, c, b in rows:
+        assert b == T.rt_chunk_bound(c, S, P), (S, P, c)
+        by.setdefault((S, P), {})[c] = b
+    for (S, P), d in by.items():
+        bs = [d[c] for c in range(P + 1)]
+        assert bs[0] == 0 and bs[-1] == S and len(bs) == P + 1
+        sizes = [bs[c + 1] - bs[c] for c in range(P)]
+        assert min(sizes) >= 1, (S, P, sizes)
+        if P >= 5 and S >= 8 * P:
+            full = sizes[:P - 3]
+            assert max(full) - min(full) <= 1
+            assert sizes[-3] < min(full) and sizes[-2] < sizes[-3] and sizes[-1] <= sizes[-2]
+    assert T.rt_chunk_bound(29, 1000, 32) == 970 and T.rt_chunk_bound(31, 1000, 32) == 995

@@ -312,6 +312,8 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.key0 = (uint32_t)p->seed;
     kp.key1 = (uint32_t)(p->seed >> 32);
     kp.chunks = rt_resolve_spp_chunks(p->spp_chunks, p->nbRayonParPixel);
+    kp.chunk_taper = !(kp.chunks < 5 || (long long)kp.S < 8ll * kp.chunks);
+    kp.chunk_den = kp.chunk_taper ? 8u * (unsigned)(kp.chunks - 3) + 7u : (unsigned)kp.chunks;
     kp.row_base = t->row_base;
     kp.tile_rows = t->tile_rows;
     kp.tile_first = t->tile_first;

@@ -1779,6 +1779,35 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
 }
 #endif
 
+// n / d and n % d for 32-bit n by a launch-constant d with m = kp's
+// floor((2^32 - 1) / d) (host, qdiv_magic): the high product is q or q - 1,
+// one remainder check fixes it (5 integer ops instead of a division).
+__device__ __forceinline__ unsigned udiv_q(unsigned n, unsigned d, unsigned m, unsigned& r)
+{
+    unsigned q = __umulhi(n, m);
+    const unsigned rr = n - q * d;
+    const bool up = rr >= d;
+    r = up ? rr - d : rr;
+    return up ? q + 1u : q;
+}
+
+// First sample of chunk c, rt.h rt_chunk_bound: w(c)*S/den with w(c) = c
+// (den = P) or the tapered weights (den = 8 (P - 3) + 7); 32-bit magic
+// division when (den + 1) * S < 2^32 (qm_chunks != 0), else 64-bit.
+__device__ __forceinline__ int chunk_start(int S, int chunks, int taper, unsigned den, unsigned qm_chunks, unsigned c)
+{
+    unsigned w = c;
+    if (taper) {
+        const unsigned P = (unsigned)chunks;
+        w = c + 3u <= P ? 8u * c : c + 2u == P ? 8u * (P - 3u) + 4u : c + 1u == P ? 8u * (P - 3u) + 6u : den;
+    }
+    if (qm_chunks != 0u) {
+        unsigned r;
+        return (int)udiv_q(w * (unsigned)S, den, qm_chunks, r);
+    }
+    return (int)(((long long)w * S) / den);
+}
+
 // Body of render_kernel (main.c semantics) and render_kernel_cuda
 // (main_cuda.cu's): one thread = (pixel, chunk of its samples).
 template <bool COUNT, bool BVH, bool SKY, bool CU>
@@ -1800,8 +1829,8 @@ __device__ __forceinline__ void render_body(const KParams& kp)
     }
     if (valid) {
         const uint32_t pixel = (uint32_t)g * (uint32_t)kp.W + (uint32_t)x;
-        const int s0 = (int)(((long long)chunk * kp.S) / kp.chunks);
-        const int s1 = (int)(((long long)(chunk + 1) * kp.S) / kp.chunks);
+        const int s0 = chunk_start(kp.S, kp.chunks, kp.chunk_taper, kp.chunk_den, 0u, (unsigned)chunk);
+        const int s1 = chunk_start(kp.S, kp.chunks, kp.chunk_taper, kp.chunk_den, 0u, (unsigned)chunk + 1u);
         __shared__ double acc_lds[(BVH ? ACC_INC : ACC_SLOTS) * 256];
         __shared__ uint32_t rng_lds[4 * 256];
         double* acc = acc_lds + threadIdx.x;
@@ -1896,27 +1925,6 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
 // atomic per lane grab was 1.8x slower (same-address atomics).  The grid is
 // the resident capacity; every lane leaves once the counter passes the
 // task count.
-// n / d and n % d for 32-bit n by a launch-constant d with m = kp's
-// floor((2^32 - 1) / d) (host, qdiv_magic): the high product is q or q - 1,
-// one remainder check fixes it (5 integer ops instead of a division).
-__device__ __forceinline__ unsigned udiv_q(unsigned n, unsigned d, unsigned m, unsigned& r)
-{
-    unsigned q = __umulhi(n, m);
-    const unsigned rr = n - q * d;
-    const bool up = rr >= d;
-    r = up ? rr - d : rr;
-    return up ? q + 1u : q;
-}
-
-// First sample of chunk c: c*S/P (exact; 32-bit when S*P < 2^32).
-__device__ __forceinline__ int chunk_start(int S, int chunks, unsigned qm_chunks, unsigned c)
-{
-    if (qm_chunks != 0u) {
-        unsigned r;
-        return (int)udiv_q(c * (unsigned)S, (unsigned)chunks, qm_chunks, r);
-    }
-    return (int)(((long long)c * S) / chunks);
-}
 
 // One lane's path in render_kernel_q: tracer's state (main.c:118-242) for
 // the sample in flight.  Rounds run in three steps so that a lane whose path
@@ -2293,8 +2301,8 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                     }
                     if (valid) {     // otherwise the lane takes its next task next round
                         pixel = (uint32_t)g * (uint32_t)K->W + (uint32_t)x;
-                        L.s = chunk_start(K->S, K->chunks, K->qm_chunks, chunk);
-                        s1 = chunk_start(K->S, K->chunks, K->qm_chunks, chunk + 1u);
+                        L.s = chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk);
+                        s1 = chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk + 1u);
 #pragma unroll
                         for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
                         owns = true;
@@ -2711,8 +2719,8 @@ int launch_render(const KParams& kp, void* stream)
         k2.qm_w = qdiv_magic((unsigned)kp.W);
         k2.qm_tile = qdiv_magic((unsigned)kp.tile_rows);
         // chunk starts c*S/P in 32 bits when (P + 1) * S fits
-        k2.qm_chunks = (unsigned long long)(kp.chunks + 1) * (unsigned long long)kp.S < (1ull << 32)
-                           ? qdiv_magic((unsigned)kp.chunks) : 0u;
+        k2.qm_chunks = (unsigned long long)(kp.chunk_den + 1) * (unsigned long long)kp.S < (1ull << 32)
+                           ? qdiv_magic(kp.chunk_den) : 0u;
         if (qbvh) queue_launch<true>(sky, ao, nb, st, k2);
         else queue_launch<false>(sky, ao, nb, st, k2);
         if (tr) {

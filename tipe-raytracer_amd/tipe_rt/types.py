@@ -12,6 +12,16 @@ def rt_resolve_spp_chunks(spp_chunks, spp):
     p = RT_SPP_CHUNKS_DEFAULT if spp_chunks == RT_SPP_CHUNKS_AUTO else spp_chunks
     return 1 if (p <= 1 or spp <= 1) else min(p, spp)
 
+
+def rt_chunk_bound(c, S, P):
+    """rt.h rt_chunk_bound: first sample of slice c of S samples in P slices
+    (equal slices, or P - 3 equal ones then three tapered, weights 8..8, 4, 2, 1)."""
+    if P < 5 or S < 8 * P:
+        return c * S // P
+    U = 8 * (P - 3) + 7
+    w = 8 * c if c <= P - 3 else 8 * (P - 3) + 4 if c == P - 2 else 8 * (P - 3) + 6 if c == P - 1 else U
+    return w * S // U
+
 (RT_CNT_SAMPLES, RT_CNT_CASTS, RT_CNT_SPHERE_TESTS, RT_CNT_SPHERE_DISC,
  RT_CNT_TRI_TESTS, RT_CNT_SHADE, RT_CNT_TEX_HITS, RT_CNT_REFRACT,
  RT_CNT_RNG_DRAWS, RT_CNT_EXACT_RESCANS, RT_CNT_BVH_NODES, RT_CNT_BVH_TRI_TESTS,
