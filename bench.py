@@ -6,7 +6,7 @@
 One step = one full frame of config C2 (README 10-sphere Cornell box,
 1200x900, 1000 spp, 6 bounces; Philox stream, seed 1010) rendered into HBM.
 With N > 1 (launched one rank per GPU by torch.distributed.run) the frame is
-split into cyclic 2-row tiles (tile t -> rank t mod N), each rank renders its
+split into cyclic 1-row tiles (row t -> rank t mod N), each rank renders its
 tiles, the tiles' colour (the canva plane: write_color_canva integers, exact
 in float32, so 12 B/px -- SURVEY §8(e)'s float3 colour payload; `--gather
 all` sends canva + albedo + normal as doubles, 72 B/px, for a denoiser) is
@@ -47,8 +47,8 @@ from tipe_rt import scenes  # noqa: E402
 
 METRIC = "Msamples/s (pixels×spp/s) at 1200×900, 1000spp, 6 bounces; 1/2/4/8 GPU"
 W, H, SPP, BOUNCES, SEED = 1200, 900, 1000, 6, 1010
-TILE_ROWS = 2        # cyclic 2-row tiles: 450 tiles, the busiest of 8 ranks renders 57 (98.7 % balance;
-                     # 8-row tiles left one rank 15 of 113, 94 %)
+TILE_ROWS = 1        # cyclic 1-row tiles: the busiest of 8 ranks renders 113 of 900 rows (99.6 % balance;
+                     # 2-row tiles: 114, 98.7 %; 8-row tiles: 120, 94 %)
 FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X FP64 vector, AMD spec (= 1/2 of the 157.3 FP32 vector peak)
 HBM_PEAK_GBS = 8000.0
 

@@ -155,7 +155,7 @@ def test_render_rows_scene_cache_tracks_content():
 
 @pytest.mark.parametrize("planes", ["all", "canva_only"])
 def test_render_rows_two_device_slots(planes):
-    """rt_init(2, {0, 0}): rt_render_rows deals cyclic 2-row tiles over two
+    """rt_init(2, {0, 0}): rt_render_rows deals cyclic 1-row tiles over two
     device slots (here both on GPU 0), copies each slot's planes back
     asynchronously and scatters the rows; only the requested planes."""
     lib = tipe_rt.lib()

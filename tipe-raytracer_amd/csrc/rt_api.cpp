@@ -910,9 +910,9 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, i
     const int W = params->largeur_image;
     const int nrows = row_hi - row_lo + 1;
     const int ndev = (int)devs.size();
-    // One device: one band.  Several: cyclic 2-row tiles (load balance: the
-    // busiest device renders at most one tile more than the average).
-    const int k = ndev == 1 ? nrows : 2;
+    // One device: one band.  Several: cyclic 1-row tiles (load balance: the
+    // busiest device renders at most one row more than the average).
+    const int k = ndev == 1 ? nrows : 1;
     const int ntiles = (nrows + k - 1) / k;
     rt_color* outs[3] = {canva, albedo, normal};
     const int nplanes = 3;

@@ -14,6 +14,7 @@ ap.add_argument("--spp", type=int, default=1000)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--chunks", type=int, default=32)
 ap.add_argument("--pipeline", action="store_true", help="alternate two streams (bench.py default)")
+ap.add_argument("--tile-rows", type=int, default=2)
 args = ap.parse_args()
 W, H = 1200, 900
 cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
@@ -22,7 +23,7 @@ ds = tipe_rt.DeviceScene(tipe_rt.make_scene(scenes.cornell_spheres()), 0)
 st = torch.cuda.current_stream().cuda_stream
 base = None
 for n in (1, 2, 4, 8):
-    t = tipe_rt.band_tiling(0, H - 1) if n == 1 else tipe_rt.cyclic_tiling(H, 2, 0, n)
+    t = tipe_rt.band_tiling(0, H - 1) if n == 1 else tipe_rt.cyclic_tiling(H, args.tile_rows, 0, n)
     rows = t.n_tiles * t.tile_rows
     nb = 2 if args.pipeline else 1
     outs = [torch.empty((3, rows, W, 3), dtype=torch.float64, device="cuda:0") for _ in range(nb)]
