@@ -65,23 +65,14 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
-#ifndef RT_BVH_SM                   // BVH kernel: resumable trace, node visits per round (0: off)
-#define RT_BVH_SM 4
-#endif
-#ifndef RT_BVH_SM_FILL              // ... and the share of lanes (eighths) that must wait to shade
-#define RT_BVH_SM_FILL 6
-#endif
 #ifndef RT_BVH_COOP                 // BVH kernel: wave-cooperative deep traversal once this many
-#define RT_BVH_COOP 1               // lanes wait for it (0: off, samples_sm)
+#define RT_BVH_COOP 1               // lanes wait for it (0: off, each lane walks its own tree)
 #endif
 #ifndef RT_FLAT                     // sphere kernel: sample loop as LanePath rounds (0: nested trace())
 #define RT_FLAT 1
 #endif
 #ifndef RT_FLAT_FILL                // ... camera rays start once this many eighths of the live lanes wait
 #define RT_FLAT_FILL 2
-#endif
-#ifndef RT_QUEUE_FILL               // queue kernel: camera rays once this many eighths of the lanes wait or lack one
-#define RT_QUEUE_FILL 4
 #endif
 #ifndef RT_QUEUE                    // sphere kernel, spp_chunks > 1: persistent lanes + (chunk, pixel) task queue
 #define RT_QUEUE 64                 // (tasks per atomic grab of a wave; 0: off)
@@ -90,18 +81,12 @@ static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) m
 #ifndef RT_WAVES_PER_SIMD_Q         // queue kernel occupancy bound
 #define RT_WAVES_PER_SIMD_Q RT_WAVES_PER_SIMD
 #endif
-#ifndef RT_PREFETCH                 // queue kernel: camera rays computed one path ahead (LDS)
-#define RT_PREFETCH 1
-#endif
 #ifndef RT_QSTATS                   // diagnostic build: round census of render_kernel_q in the trace
 #define RT_QSTATS 0
 #endif
 #define RT_TRACE_WORDS (RT_QSTATS ? 18 : 4)
 #ifndef RT_QB_STEPS                 // queue kernel, BVH scenes: node visits per lane and round
 #define RT_QB_STEPS 3
-#endif
-#ifndef RT_NRM_RSQ                  // normalize: 1/|a| refined from the sqrt sequence's own rsq (no v_rcp_f64)
-#define RT_NRM_RSQ 1
 #endif
 #ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
 #define RT_WAVES_PER_SIMD_BVH 3
@@ -132,13 +117,8 @@ __device__ __forceinline__ V3 normalize(V3 a)
     const double n2 = dot(a, a);
     const double mn = fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
     if (n2 >= 0x1p-760 && n2 <= 0x1p760 && mn >= 0x1p-900) {
-#if RT_NRM_RSQ
-        double L, rc;
+        double L, rc;                    // 1/L from the sqrt sequence's own rsq (rt_device_math.h)
         sqrt_rcp_core(n2, L, rc);
-#else
-        const double L = sqrt_core(n2);
-        const double rc = rcp_refined(L);
-#endif
         return v3(div_core(a.x, L, rc), div_core(a.y, L, rc), div_core(a.z, L, rc));
     }
     return divs(a, sqrt(n2));
@@ -1180,11 +1160,10 @@ __device__ __forceinline__ void camera_ray(const KParams& kp, int x, int g, ST& 
 //   SM_CAST    runs the sphere half of the next cast and sets up traversal,
 //   SM_TRAV    visits nodes of the triangle BVH,
 // and a lane's casts, draws and sums happen in the same order as in trace(),
-// so results are bit-identical.  samples_sm runs it (RT_BVH_SM > 0): every
-// round each lane runs its phase, at most RT_BVH_SM node visits; a lane
-// whose traversal is short moves on to its next cast instead of idling until
-// the wave's longest traversal ends.  C4: 357 -> 422 Msamples/s, traversal
-// lane slots 258 -> 97 per sample (RT_BVH_SM 4, RT_BVH_SM_FILL 6).
+// so results are bit-identical.  samples_coop runs it (the fixed-grid BVH
+// kernel: spp_chunks 1, trees too deep for the queue kernel's stacks); r01's
+// samples_sm (each lane at most 4 node visits per round) is superseded by the
+// queue kernel's resumable walks (render_kernel_q<.., BVH>).
 enum : int { SM_RESOLVE = 0, SM_CAM = 1, SM_CAST = 2, SM_TRAV = 3, SM_DONE = 4 };
 
 // AOM: AO compiled out (0), always on (1), or read from kp.useAO (2); the
@@ -1465,26 +1444,6 @@ struct LanePath {
     }
 };
 
-#if RT_BVH_SM > 0
-template <bool COUNT, bool SKY>
-__device__ __forceinline__ void samples_sm(const KParams& kp, int x, int g, uint32_t pixel, int s0, int s1,
-                                           uint32_t* rng, double* acc, Cnt& cnt)
-{
-    unsigned short* stk = bvh_stack();
-    LanePath<COUNT, SKY> L;
-    L.init(s0, s1);
-    while (L.state != SM_DONE) {
-        // shade/start/cast only once enough of the wave waits for it (in
-        // eighths of its live lanes, RT_BVH_SM_FILL); else traverse on
-        const unsigned long long live = __ballot(1), wait = __ballot(L.state != SM_TRAV);
-        const bool go = wait == live || __popcll(wait) * 8 >= __popcll(live) * RT_BVH_SM_FILL;
-        if (go && L.state == SM_RESOLVE) L.resolve(kp, acc, cnt);
-        if (go && L.state == SM_CAM) L.start(kp, x, g, pixel, s1, rng, acc, cnt);
-        if (go && L.state == SM_CAST) L.cast(kp, cnt);
-        if (L.state == SM_TRAV) L.trav(kp, stk, RT_BVH_SM, cnt);
-    }
-}
-#endif
 
 
 #if RT_FLAT > 0
@@ -1843,10 +1802,6 @@ __device__ __forceinline__ void render_body(const KParams& kp)
 #if RT_BVH_COOP > 0
         if constexpr (BVH && !CU) {
             samples_coop<COUNT, SKY>(kp, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc, cnt);
-        } else
-#elif RT_BVH_SM > 0
-        if constexpr (BVH && !CU) {
-            samples_sm<COUNT, SKY>(kp, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc, cnt);
         } else
 #endif
 #if RT_FLAT > 0
