@@ -62,7 +62,12 @@ for f in ["bench.json", "host_path.json", "pytest_gpu.log", "demo.log"]:
     p = os.path.join(src, f)
     if os.path.exists(p):
         os.system("cp %s %s" % (p, os.path.join(dst, f)))
+import subprocess
+commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
 json.dump({"render_kernel_hbm_bytes_per_launch": hbm, "source": dst + "/summary.json",
-           "workload": "C2 1200x900 1000spp 6 bounces, spp_chunks 32"},
+           "workload": "C2 1200x900 1000spp 6 bounces, spp_chunks 32", "kernel": KNAME,
+           "measured_at_commit": commit,
+           "note": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, separate passes; a committed profile "
+                   "value, re-measured by tools/profile_run.sh + tools/summarize_pmc.py"},
           open(os.path.join("profiles", "pmc_traffic.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
