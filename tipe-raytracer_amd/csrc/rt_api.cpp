@@ -698,7 +698,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     // triangle arrays are then stored in leaf order.  r_scene bounds every
     // coordinate a ray origin can take on the scene's surfaces.
     BvhBuild bvh;
-    if (scene->nbTriangles > 32) {
+    if (scene->nbTriangles > 32) {           // (a BVH over C3's 5 triangles: 5118 -> 4482 Msamples/s)
         double r = 1.0;
         for (int i = 0; i < scene->nbSpheres; ++i) {
             const rt_sphere& q = scene->sphere_list[i];

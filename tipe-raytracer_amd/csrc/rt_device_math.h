@@ -186,17 +186,25 @@ __device__ __forceinline__ int pm_sincos(float x, double& s, double& c)
                                           KCV(b, KC_C3)), KCV(b, KC_C2)), KCV(b, KC_C1));
     s = fma(r * z, ps, r);
     c = fma(z * z, pc, fma(-0.5, z, 1.0));
-    return (int)((long long)kd & 3);
+    // kd is an integer-valued double of small magnitude (|x| <= 2^27 here:
+    // the sampler's x <= 2 pi), so the 32-bit conversion is exact
+    return (int)kd & 3;
 }
 
+// Quadrant q of the reduced argument: sin x = (s, c, -s, -c)[q], cos x =
+// (c, -s, -c, s)[q].  Rounding to float commutes with negation (round to
+// nearest is symmetric), so the pair is rounded first and the quadrant is
+// applied to the floats: one swap and two sign flips.
 __device__ __forceinline__ void pm_sincosf(float x, float& sn, float& cs)
 {
     double s, c;
     const int q = pm_sincos(x, s, c);
-    const double vs = (q == 0) ? s : (q == 1) ? c : (q == 2) ? -s : -c;
-    const double vc = (q == 0) ? c : (q == 1) ? -s : (q == 2) ? -c : s;
-    sn = (float)vs;
-    cs = (float)vc;
+    const float fs = (float)s, fc = (float)c;
+    const bool odd = (q & 1) != 0;
+    const float a = odd ? fc : fs, b = odd ? fs : fc;
+    const unsigned ns = (unsigned)(q & 2) << 30, nc = (unsigned)((q + 1) & 2) << 30;
+    sn = __uint_as_float(__float_as_uint(a) ^ ns);
+    cs = __uint_as_float(__float_as_uint(b) ^ nc);
 }
 
 // Exact f64 sqrt and division without their range fixups.  These are the
