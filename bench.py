@@ -467,7 +467,7 @@ def main():
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": FP64_VECTOR_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / FP64_VECTOR_PEAK_TFLOPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "traffic_model_bytes_per_launch": traffic_model, "kernel": "render_kernel_q<false, 0, false> (persistent task queue; no sky, no AO, no BVH) + combine_kernel",
+                         "traffic_model_bytes_per_launch": traffic_model, "kernel": "render_kernel_q<false, 0, 0> (persistent task queue; no sky, no AO, no BVH) + combine_kernel",
                          "kernel_ms": round(kernel_ms, 3), "flops_per_launch": flops,
                          "flops_per_sample": round(flops / launch_samples, 1),
                          "note": "achieved = algorithmic FLOPs of the work done (SURVEY 8d formula on the "

@@ -87,6 +87,7 @@ struct KParams {
     double bvh_srel, bvh_sabs;   // distance-cull slack (rt_bvh.cpp)
     float bvh_rbox;              // >= |every bound| of the tree's boxes (single-precision slab margin)
     int bvh_stack;               // traversal stack entries the tree can need (3 * depth4 + 1)
+    int bvh_steps;               // queue kernel: node visits per lane and round (host: by tree depth)
     int ns, ns_pad, nt;
     int tw, th;
     long long n_texels;

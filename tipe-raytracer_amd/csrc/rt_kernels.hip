@@ -85,9 +85,6 @@ static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) m
 #define RT_QSTATS 0
 #endif
 #define RT_TRACE_WORDS (RT_QSTATS ? 18 : 4)
-#ifndef RT_QB_STEPS                 // queue kernel, BVH scenes: node visits per lane and round
-#define RT_QB_STEPS 3
-#endif
 #ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
 #define RT_WAVES_PER_SIMD_BVH 3
 #endif
@@ -1163,7 +1160,7 @@ __device__ __forceinline__ void camera_ray(const KParams& kp, int x, int g, ST& 
 // so results are bit-identical.  samples_coop runs it (the fixed-grid BVH
 // kernel: spp_chunks 1, trees too deep for the queue kernel's stacks); r01's
 // samples_sm (each lane at most 4 node visits per round) is superseded by the
-// queue kernel's resumable walks (render_kernel_q<.., BVH>).
+// queue kernel's resumable walks (render_kernel_q<.., QB>).
 enum : int { SM_RESOLVE = 0, SM_CAM = 1, SM_CAST = 2, SM_TRAV = 3, SM_DONE = 4 };
 
 // AOM: AO compiled out (0), always on (1), or read from kp.useAO (2); the
@@ -2111,7 +2108,7 @@ struct QPath {
     }
 };
 
-template <bool SKY, int AOM, bool BVH>
+template <bool SKY, int AOM, int QB>
 __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
 {
     __shared__ double acc_lds[ACC_INC * 256];
@@ -2157,8 +2154,8 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
         qs[1] += (unsigned long long)__popcll(__ballot(L.state == SM_CAST));
 #endif
         // ---- 1. closest hit (main.c:52-92) for every lane with a ray ------
-        if (BVH) {
-            // spheres, then the triangle BVH: up to RT_QB_STEPS node visits
+        if (QB > 0) {
+            // spheres, then the triangle BVH: up to QB node visits
             // per round; a deeper walk resumes next round (its lane skips
             // the path work meanwhile), so a wave never waits for its
             // deepest lane's whole walk
@@ -2177,7 +2174,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 const Ray32 r32 = ray32(L.o, dd, kp.bvh_rbox);
                 unsigned short* stk = bvh_stack_q();
 #pragma unroll 1
-                for (int j = 0; j < RT_QB_STEPS; ++j) {
+                for (int j = 0; j < QB; ++j) {
 #if RT_QSTATS
                     qs[6] += 1;
                     qs[7] += (unsigned long long)__popcll(__ballot(L.state == SM_TRAV));
@@ -2601,36 +2598,37 @@ static void launch_variant(const KParams& kp_in, void* stream)
 }
 
 #if RT_QUEUE > 0
-template <bool SKY, int AOM, bool BVH>
+template <bool SKY, int AOM, int QB>
 static void queue_occupancy(int& nb)
 {
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<SKY, AOM, BVH>, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<SKY, AOM, QB>, 256, 0);
 }
 
 // Resident blocks of the queue kernel on this device (grid of render_kernel_q).
 // Cached per device and variant; rt_fill_canva may run on several host
 // threads at once (main.c's pthreads), so the cache is atomic (every thread
 // computes the same value).
-template <bool BVH>
+template <int QB>
 static void queue_occupancy_v(bool sky, bool ao, int& nb)
 {
-    if (sky && ao) queue_occupancy<true, AO_ON, BVH>(nb);
-    else if (sky) queue_occupancy<true, AO_OFF, BVH>(nb);
-    else if (ao) queue_occupancy<false, AO_ON, BVH>(nb);
-    else queue_occupancy<false, AO_OFF, BVH>(nb);
+    if (sky && ao) queue_occupancy<true, AO_ON, QB>(nb);
+    else if (sky) queue_occupancy<true, AO_OFF, QB>(nb);
+    else if (ao) queue_occupancy<false, AO_ON, QB>(nb);
+    else queue_occupancy<false, AO_OFF, QB>(nb);
 }
-static unsigned queue_grid(bool sky, bool ao, bool bvh)
+static unsigned queue_grid(bool sky, bool ao, int qb)
 {
-    static std::atomic<int> cached[8][64];
+    static std::atomic<int> cached[12][64];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + (bvh ? 4 : 0)][dev & 63];
+    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? 1 : 2)][dev & 63];
     int c = slot.load(std::memory_order_relaxed);
     if (c <= 0) {
         int nb = 0, ncu = 0;
-        if (bvh) queue_occupancy_v<true>(sky, ao, nb);
-        else queue_occupancy_v<false>(sky, ao, nb);
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (qb == 0) queue_occupancy_v<0>(sky, ao, nb);
+        else if (qb == 3) queue_occupancy_v<3>(sky, ao, nb);
+        else queue_occupancy_v<4>(sky, ao, nb);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         c = std::max(1, nb) * std::max(1, ncu);
         if (std::getenv("RT_QUEUE_VERBOSE")) std::fprintf(stderr, "render_kernel_q: %d blocks/CU x %d CUs -> %d\n", nb, ncu, c);
         slot.store(c, std::memory_order_relaxed);
@@ -2641,13 +2639,13 @@ static unsigned queue_grid(bool sky, bool ao, bool bvh)
     return (unsigned)c;
 }
 
-template <bool BVH>
+template <int QB>
 static void queue_launch(bool sky, bool ao, unsigned nb, hipStream_t st, const KParams& k2)
 {
-    if (sky && ao) hipLaunchKernelGGL((render_kernel_q<true, AO_ON, BVH>), dim3(nb), dim3(256), 0, st, k2);
-    else if (sky) hipLaunchKernelGGL((render_kernel_q<true, AO_OFF, BVH>), dim3(nb), dim3(256), 0, st, k2);
-    else if (ao) hipLaunchKernelGGL((render_kernel_q<false, AO_ON, BVH>), dim3(nb), dim3(256), 0, st, k2);
-    else hipLaunchKernelGGL((render_kernel_q<false, AO_OFF, BVH>), dim3(nb), dim3(256), 0, st, k2);
+    if (sky && ao) hipLaunchKernelGGL((render_kernel_q<true, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
+    else if (sky) hipLaunchKernelGGL((render_kernel_q<true, AO_OFF, QB>), dim3(nb), dim3(256), 0, st, k2);
+    else if (ao) hipLaunchKernelGGL((render_kernel_q<false, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
+    else hipLaunchKernelGGL((render_kernel_q<false, AO_OFF, QB>), dim3(nb), dim3(256), 0, st, k2);
 }
 
 // floor((2^32 - 1) / d) for udiv_q
@@ -2657,12 +2655,15 @@ static unsigned qdiv_magic(unsigned d) { return d ? (unsigned)(0xffffffffull / d
 int launch_render(const KParams& kp, void* stream)
 {
 #if RT_QUEUE > 0
-    const bool qbvh = kp.bvh != nullptr && RT_QB_STEPS > 0 && kp.bvh_stack <= kStackQ;
+    const bool qbvh = kp.bvh != nullptr && kp.bvh_stack <= kStackQ;
     if (kp.task_ctr && kp.chunks > 1 && (!kp.bvh || qbvh) && !kp.cuda && !kp.sums) {
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
-        const unsigned nb = queue_grid(sky, ao, qbvh);
+        // node visits per lane and round: 4 for shallow trees, 3 for deep ones
+        // (kp.bvh_steps, host; compile-time per instantiation)
+        const int qb = qbvh ? (kp.bvh_steps <= 3 ? 3 : 4) : 0;
+        const unsigned nb = queue_grid(sky, ao, qb);
         unsigned long long* tr = nullptr;
         const char* tf = std::getenv("RT_QUEUE_TRACE");
         if (tf) (void)hipMalloc((void**)&tr, (size_t)nb * 256 * RT_TRACE_WORDS * sizeof(unsigned long long));
@@ -2676,8 +2677,9 @@ int launch_render(const KParams& kp, void* stream)
         // chunk starts c*S/P in 32 bits when (P + 1) * S fits
         k2.qm_chunks = (unsigned long long)(kp.chunk_den + 1) * (unsigned long long)kp.S < (1ull << 32)
                            ? qdiv_magic(kp.chunk_den) : 0u;
-        if (qbvh) queue_launch<true>(sky, ao, nb, st, k2);
-        else queue_launch<false>(sky, ao, nb, st, k2);
+        if (qb == 3) queue_launch<3>(sky, ao, nb, st, k2);
+        else if (qb == 4) queue_launch<4>(sky, ao, nb, st, k2);
+        else queue_launch<0>(sky, ao, nb, st, k2);
         if (tr) {
             std::vector<unsigned long long> h((size_t)nb * 256 * RT_TRACE_WORDS);
             (void)hipStreamSynchronize(st);
