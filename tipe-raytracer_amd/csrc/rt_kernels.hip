@@ -706,6 +706,15 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
 #endif
     } else {
         for (int k = 0; k < kp.nt; ++k) tri_test<COUNT, CU>(kp, k, o, d, best, kind, win, win_orig);
+#ifdef RT_DUP_SCAN
+        {
+            double b2 = best;
+            int k2 = kind, w2 = win, o2 = win_orig;
+            for (int k = 0; k < kp.nt; ++k)
+                tri_test<COUNT, CU>(kp, k, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2);
+            if (opaque_false()) { best = b2; kind = k2; win = w2; win_orig = o2; }
+        }
+#endif
     }
     t_best = best;
     idx = win;
