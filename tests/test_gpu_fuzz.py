@@ -29,7 +29,7 @@ def _zero_some(rng, c, zeros):
     return tuple(0.0 if rng.random() < 0.35 else float(x) for x in c)
 
 
-def random_scene(seed, zeros=False, chunks=None):
+def random_scene(seed, zeros=False, chunks=None, nt_range=None, spp=None):
     rng = np.random.default_rng(seed)
     ns = int(rng.integers(1, 14))
     sph = (Sphere * ns)()
@@ -53,8 +53,10 @@ def random_scene(seed, zeros=False, chunks=None):
         sph[k].radius = r
         sph[k].mat = scenes.material(diff, em, es, refl, alpha, ior)
     mesh = None
-    if rng.random() < 0.7:
+    if nt_range is not None or rng.random() < 0.7:
         nt = int(rng.integers(40, 120)) if seed % 2 else int(rng.integers(1, 20))
+        if nt_range is not None:
+            nt = int(rng.integers(*nt_range))
         tris = (Triangle * nt)()
         nm, tw, th = 5, int(rng.integers(1, 5)), int(rng.integers(1, 5))
         qm = (C.c_int * nt)(*[int(x) for x in rng.integers(0, nm, nt)])
@@ -79,6 +81,8 @@ def random_scene(seed, zeros=False, chunks=None):
     if chunks is not None:
         p.spp_chunks = chunks
         p.nbRayonParPixel = max(p.nbRayonParPixel, chunks)
+    if spp is not None:
+        p.nbRayonParPixel = spp
     return bundle, p
 
 
@@ -106,4 +110,18 @@ def test_random_scene_cuda_semantics_bitexact(seed):
     if bundle.mesh is not None:
         scenes.with_cuda_materials(bundle.mesh)
     p.semantics = tipe_rt.types.RT_SEM_CUDA
+    check_parity(bundle, p)
+
+
+@pytest.mark.parametrize("seed", range(300, 324))
+def test_random_bvh_scene_queue_tiny_grid_bitexact(seed, monkeypatch):
+    """Random 100-400 triangle meshes (BVH) with random spheres, through the
+    BVH task-queue kernel (resumable walks, rt_kernels.hip render_kernel_q<..,
+    QB>) on a 1-3 block grid, so every lane runs many tasks and walks span
+    rounds across task switches; 5-6 sample slices at 40-48 spp use the
+    tapered slice bounds (rt_chunk_bound).  Bit for bit vs the oracle."""
+    monkeypatch.setenv("RT_QUEUE_BLOCKS", str(1 + seed % 3))
+    bundle, p = random_scene(seed, zeros=bool(seed % 2), chunks=5 + seed % 2, nt_range=(100, 400),
+                             spp=40 + 8 * (seed % 2))
+    p.largeur_image, p.hauteur_image = min(p.largeur_image, 20), min(p.hauteur_image, 15)
     check_parity(bundle, p)
