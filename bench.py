@@ -116,8 +116,8 @@ def cpu_baseline(scene, cam, threads=12):
                 main.c's threads share it (lock-serialised; libm math);
       fair:     a lock-free stream per pixel (Philox; portable math).
     Msamples/s does not depend on spp (pixels are independent), so each leg
-    renders the 1200x900 frame at 1-8 spp (about 1-14 s each on the GPU
-    box's 16-CPU share).  The headline is fair x 12."""
+    renders the 1200x900 frame at 1-32 spp (about 1-14 s each on the GPU
+    box's 16-CPU share).  The headline is fair x 12 at 32 spp."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi
     o = oracle_ffi.oracle()
@@ -126,7 +126,9 @@ def cpu_baseline(scene, cam, threads=12):
     legs = {}
     for mode, rng in (("fair", tipe_rt.RT_RNG_PHILOX), ("faithful", tipe_rt.RT_RNG_GLIBC)):
         for nt in sorted({1, threads, share}):
-            spp = (8 if nt > 1 else 2) if mode == "fair" else (2 if nt == 1 else 1)
+            # the headline leg (fair, `threads`) renders 32 spp (~5 s on 12 threads); the
+            # others 1-8 spp, so the six legs take about 45 s together
+            spp = (32 if nt == threads else 8 if nt > 1 else 2) if mode == "fair" else (2 if nt == 1 else 1)
             p = tipe_rt.make_params(W, H, spp, BOUNCES, cam, focus=3.0, seed=SEED, rng=rng, chunks=1)
             t0 = time.perf_counter()
             rc = o.oracle_render_rows(C.byref(scene), C.byref(p), H - 1, 0, nt, 1, canva.ctypes.data,
