@@ -341,6 +341,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
         // do best with 3 (measured: sweep depth4 3: 3395 -> 3542 at 4; C4 depth4 7:
         // 1134 at 3, 1122 at 4)
         kp.bvh_steps = sc->bvh_depth <= 4 ? 4 : 3;
+        kp.bvh_nodes = sc->bvh_nodes;
     }
     return RT_OK;
 }

@@ -288,6 +288,28 @@ bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
     for (int i = 0; i < nt; ++i) out.order[(size_t)i] = P[(size_t)i].idx;
     out.depth = bld.max_depth;
     collapse(out.nodes, 0, out.nodes4, 0, out.depth4);
+    // Breadth-first node order: the top levels are the first nodes (the queue
+    // kernel keeps the first ones in LDS).  Child indices are renumbered.
+    {
+        const size_t n4 = out.nodes4.size();
+        std::vector<int> order;                  // new position -> old index
+        order.reserve(n4);
+        order.push_back(0);
+        for (size_t h = 0; h < order.size(); ++h) {
+            const BvhNode4& nd = out.nodes4[(size_t)order[h]];
+            for (int c = 0; c < 4; ++c)
+                if (nd.count[c] == 0) order.push_back(nd.child[c]);
+        }
+        std::vector<int> pos(n4, -1);
+        for (size_t i = 0; i < order.size(); ++i) pos[(size_t)order[i]] = (int)i;
+        std::vector<BvhNode4> bfs(order.size());
+        for (size_t i = 0; i < order.size(); ++i) {
+            bfs[i] = out.nodes4[(size_t)order[i]];
+            for (int c = 0; c < 4; ++c)
+                if (bfs[i].count[c] == 0) bfs[i].child[c] = pos[(size_t)bfs[i].child[c]];
+        }
+        out.nodes4.swap(bfs);
+    }
     if (3 * out.depth4 + 1 > kStack4 || out.nodes4.size() >= 65535) {
         out = BvhBuild();
         return false;

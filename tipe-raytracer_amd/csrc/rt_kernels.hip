@@ -476,6 +476,16 @@ __device__ __forceinline__ unsigned short* bvh_stack_q()
     __shared__ unsigned short stkq_lds[kStackQ * 256];
     return stkq_lds + threadIdx.x;
 }
+// ... and the block's copy of the tree's top nodes (RT_QB_TOP x 128 B; the
+// block then needs <= 40 KiB of LDS, still 4 blocks per CU)
+#ifndef RT_QB_TOP
+#define RT_QB_TOP 40
+#endif
+__device__ __forceinline__ BvhNode4* bvh_top_q()
+{
+    __shared__ BvhNode4 top_lds[RT_QB_TOP > 0 ? RT_QB_TOP : 1];
+    return top_lds;
+}
 // Conservative single-precision slab test (the culling only has to be a
 // superset of the double test on the padded boxes).  Per ray
 // and axis: inv = rcp((float)d) (|d| clamped to >= 2^-60; <= 2 ulp of 1/d),
@@ -545,12 +555,14 @@ __device__ __forceinline__ void box4(const KParams& kp, const BvhNode4* nd, cons
 // the next node (nearest hit internal child, else the stack top).  Returns
 // false when the traversal is over.  tris_bvh loops it to the end; the
 // resumable trace (render_sm) runs a bounded number of visits per round.
-template <bool COUNT, bool CU>
+template <bool COUNT, bool CU, int NTOP = 0>
 __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3 d, const Ray32& r32,
                                          unsigned short* stk, int& node, int& sp, double& best, int& kind,
-                                         int& win, int& win_orig, Cnt& cnt)
+                                         int& win, int& win_orig, Cnt& cnt, const BvhNode4* top = nullptr)
 {
-    const BvhNode4* nd = kp.bvh + node;
+    // NTOP > 0: the first NTOP nodes (breadth-first: the top levels) are read
+    // from the block's LDS copy `top`, the rest from HBM/L2
+    const BvhNode4* nd = (NTOP > 0 && node < NTOP) ? top + node : kp.bvh + node;
     if (COUNT) {
         cnt.c[RT_CNT_BVH_NODES] += 1;
         wave_slots(cnt, RT_CNT_BVH_LANE_SLOTS);
@@ -2139,6 +2151,16 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
     Stream st;                       // draw stream of the sample in flight (next31 for refraction / AO)
     st.start(0u, 0u, kp.key0, kp.key1, rng);
+    // shallow trees (QB 4: depth4 <= 4, e.g. the 50-node sweep tree) keep
+    // their top nodes in LDS: sweep +5.7 %; deep ones gain nothing (C4 -0.5 %)
+    constexpr int NTOP = QB == 4 ? RT_QB_TOP : 0;
+    if (NTOP > 0) {                          // the tree's top nodes into LDS, once per block
+        float4* dst = (float4*)bvh_top_q();
+        const float4* src = (const float4*)kp.bvh;
+        const int n = min(NTOP, kp.bvh_nodes) * (int)(sizeof(BvhNode4) / sizeof(float4));
+        for (int i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+        __syncthreads();
+    }
     const long long t_start = kp.trace ? wall_clock64() : 0;
     unsigned rounds = 0, ntasks = 0;
 #if RT_QSTATS
@@ -2182,6 +2204,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 const V3 dd = L.cast_dir();
                 const Ray32 r32 = ray32(L.o, dd, kp.bvh_rbox);
                 unsigned short* stk = bvh_stack_q();
+                const BvhNode4* top = NTOP > 0 ? bvh_top_q() : nullptr;
 #pragma unroll 1
                 for (int j = 0; j < QB; ++j) {
 #if RT_QSTATS
@@ -2190,8 +2213,8 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
 #endif
                     if (L.state == SM_TRAV) {
                         Cnt cnt;
-                        if (!bvh_step<false, false>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind, L.win, win_orig,
-                                                    cnt))
+                        if (!bvh_step<false, false, NTOP>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind, L.win,
+                                                           win_orig, cnt, top))
                             L.state = SM_RESOLVE;
                     }
                     if (__ballot(L.state == SM_TRAV) == 0ull) break;
