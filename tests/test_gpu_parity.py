@@ -116,8 +116,11 @@ def test_device_normalize_fast_path_is_ieee():
 
 def test_device_normalize_stress():
     """normalize()'s fast path (sqrt_rcp_core: 1/|a| refined from the sqrt
-    sequence's rsq, then div_core) equals IEEE a / sqrt(a.a) bit for bit on
-    2^32 pseudo-random vectors (directions, n + dir sums, scales 2^-450..2^450)."""
+    sequence's rsq, then div_core) and its seeded forms equal IEEE
+    a / sqrt(a.a) bit for bit on 2^32 pseudo-random vectors: directions, n + dir
+    sums, scales 2^-450..2^450 (normalize), the sampler's float-built unit
+    vectors (normalize_unit, series seed) and sphere hit offsets hp - C
+    (normalize_sph, radius seed), a quarter each of the last two."""
     fast, bad = tipe_rt.verify_normalize(seed=20261016, n=1 << 32)
     assert bad == 0
     assert fast > (1 << 31)

@@ -248,6 +248,31 @@ __device__ __forceinline__ void sqrt_rcp_core(double x, double& L, double& rc)  
     const double r0 = h + h;
     rc = fma(r0, fma(-L, r0, 1.0), r0);
 }
+// sqrt_rcp_core for x within 2^-18 of 1 (the sampler's float-built unit
+// vectors), without v_rsq_f64: e = x - 1 is exact (Sterbenz) and the series
+// y = 1 - e/2 + 3e^2/8 is 1/sqrt(x) within 5|e|^3/16 (<= 2^-55.7) plus its
+// rounding; then sqrt_core's shape: g = x y, h = y/2, and one Newton step
+// L = g + (x - g^2) h.  L == sqrt(x) for EVERY double in [1 - 2^-18, 1 + 2^-18]
+// (5.2e10 values, tools/check_near1.sh; tests/test_near1_sqrt.py checks a
+// sample and the neighbourhood of 1).  rc: one Newton step on y (within
+// 2^-51 of 1/L) leaves it within 2^-100 + half an ulp of 1/L, div_core's
+// precondition.
+__device__ __forceinline__ void sqrt_rcp_near1(double x, double& L, double& rc)   // |x - 1| <= 2^-18
+{
+    const double e = x - 1.0;
+    const double y = fma(fma(e, 0.375, -0.5), e, 1.0);
+    const double g = x * y, h = 0.5 * y;
+    L = fma(fma(-g, g, x), h, g);
+    rc = fma(y, fma(-L, y, 1.0), y);
+}
+// div_core that also keeps the sign of a zero x (x = -0: -0, as IEEE x / d
+// for d > 0): the residual is formed as d q - x and subtracted, which gives
+// the same rounded value as div_core for every x != 0.
+__device__ __forceinline__ double div_core0(double x, double d, double rc)  // x = +-0 or |x| in [2^-900, 2^900]
+{
+    const double q = x * rc;
+    return fma(-fma(d, q, -x), rc, q);
+}
 __device__ __forceinline__ double rcp_refined(double d)         // d in [2^-400, 2^400]
 {
     double rc = __builtin_amdgcn_rcp(d);

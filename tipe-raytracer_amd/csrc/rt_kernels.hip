@@ -121,6 +121,17 @@ __device__ __forceinline__ V3 normalize(V3 a)
     return divs(a, sqrt(n2));
 }
 
+// normalize() of random_dir_no_norm's vector (rtutility.h:198-202): the
+// components are float products, each nonzero (cos/sin of a float are never 0)
+// or a signed zero (theta = 0: sin = +0), and |a|^2 is within 6 * 2^-24 of 1,
+// so no range guard: sqrt_rcp_near1 and div_core0 on every lane.
+__device__ __forceinline__ V3 normalize_unit(V3 a)
+{
+    double L, rc;
+    sqrt_rcp_near1(dot(a, a), L, rc);
+    return v3(div_core0(a.x, L, rc), div_core0(a.y, L, rc), div_core0(a.z, L, rc));
+}
+
 // The kernel's by-value parameters (kernarg segment) through an address the
 // compiler cannot see through: fields read via it are loaded (s_load) where
 // they are used instead of being held in SGPRs -- and spilled to VGPR lanes,
@@ -800,13 +811,10 @@ __device__ __forceinline__ void sky_material(const KParams& kp, int idx, const S
     mat.alpha = 1.0;
 }
 
-// random_dir_no_norm, rtutility.h:189-203 (float sinf/cosf of double args)
-template <bool COUNT>
-__device__ __forceinline__ V3 random_dir(Stream& st, Cnt& cnt)
+// random_dir_no_norm's vector before its normalize, rtutility.h:192-200
+// (float sinf/cosf of double args), from its two draws u, v
+__device__ __forceinline__ V3 sampler_vec(double u, double v)
 {
-    if (COUNT) cnt.c[RT_CNT_SHADE] += 1;
-    const double u = unit31(st.next31());
-    const double v = unit31(st.next31());
     const double theta = 0x1.921fb54442d18p+2 * u;        // 2*PI*u
     const double xv = 2 * v - 1;                          // phi = acos(2v - 1): only (float)phi is used
     float st_, ct_, sp_, cp_;
@@ -830,14 +838,24 @@ __device__ __forceinline__ V3 random_dir(Stream& st, Cnt& cnt)
         st_ = f ? a : st_; ct_ = f ? b : ct_;
     }
 #endif
-    const V3 dir = v3((double)(ct_ * sp_), (double)(st_ * sp_), (double)cp_);
+    return v3((double)(ct_ * sp_), (double)(st_ * sp_), (double)cp_);
+}
+
+// random_dir_no_norm, rtutility.h:189-203
+template <bool COUNT>
+__device__ __forceinline__ V3 random_dir(Stream& st, Cnt& cnt)
+{
+    if (COUNT) cnt.c[RT_CNT_SHADE] += 1;
+    const double u = unit31(st.next31());
+    const double v = unit31(st.next31());
+    const V3 dir = sampler_vec(u, v);
 #ifdef RT_DUP_NORMALIZE
     {
-        const V3 a = normalize(dir), b = normalize(v3(launder(dir.x), launder(dir.y), launder(dir.z)));
+        const V3 a = normalize_unit(dir), b = normalize_unit(v3(launder(dir.x), launder(dir.y), launder(dir.z)));
         return opaque_false() ? b : a;
     }
 #endif
-    return normalize(dir);
+    return normalize_unit(dir);
 }
 
 // refracted_vec, rtutility.h:210-227 (indices squared: reference quirk)
@@ -1048,7 +1066,7 @@ __device__ __forceinline__ bool cuda_hit(const KParams& kp, const V3 o, const V3
     hp = o + muls(d, t);                                 // ray_at
     if (kind == HIT_SPHERE) {
         const SphGeo s = kp.sph[idx];
-        hn = normalize(hp - v3(s.cx, s.cy, s.cz));       // sphere.hu:31,40
+        hn = normalize(hp - v3(s.cx, s.cy, s.cz));   // sphere.hu:31,40
         mat = load_mat(kp.sph_mat + idx);
     } else {
         const TriGeo g = kp.tri[idx];
@@ -2365,15 +2383,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 // random_dir_no_norm (rtutility.h:189-203), then n + dir (main.c:163)
                 const double u = unit31(wa >> 1);
                 const double v = unit31(wb >> 1);
-                const double theta = 0x1.921fb54442d18p+2 * u;        // 2*PI*u
-                const double xv = 2 * v - 1;                          // phi = acos(2v - 1)
-                float st_, ct_, sp_, cp_;
-                if (!phi_sincosf_fast(xv, sp_, cp_)) {
-                    const double phi = pm_acos(xv);
-                    pm_sincosf((float)phi, sp_, cp_);
-                }
-                pm_sincosf((float)theta, st_, ct_);
-                X = H.hn + normalize(v3((double)(ct_ * sp_), (double)(st_ * sp_), (double)cp_));
+                X = H.hn + normalize_unit(sampler_vec(u, v));
                 st.n += 2;
             }
             const V3 dn = normalize(X);
@@ -2804,11 +2814,17 @@ __global__ __launch_bounds__(256) void verify_spheres_kernel(const KParams kp, c
     }
 }
 
-// normalize() (fast lanes: sqrt_rcp_core / rcp_refined + div_core) against
-// IEEE a / sqrt(a.a) on n pseudo-random vectors (Philox, key = seed): half
-// unit-scale (directions and n + dir sums), a quarter with one common scale
-// 2^e, e in [-400, 400), a quarter with independent per-component scales.
-// counts[0] += vectors on the fast path, counts[1] += results that differ.
+// normalize() (fast lanes: sqrt_rcp_core / rcp_refined + div_core) and its
+// seeded forms against IEEE a / sqrt(a.a) on n pseudo-random vectors (Philox,
+// key = seed), by q.w2 & 7:
+//   0-3  normalize(): unit-scale vectors, n + dir sums, one common scale 2^e
+//        (e in [-400, 400)), a scale per component
+//   4-5  normalize_unit() on the sampler's vectors (sampler_vec of two 31-bit
+//        draws, as random_dir makes them)
+//   6-7  normalize() on hit-point offsets hp - C: C with components
+//        scaled by 2^[-8, 12), |r| = 2^[-10, 10) times [1, 2), hp = C + r u for a
+//        random unit u (rounded, as a hit point is), seeded as the host does
+// counts[0] += vectors on a fast path, counts[1] += results that differ.
 __device__ __forceinline__ double vn_comp(uint32_t hi, uint32_t lo)
 {
     const unsigned long long m = ((unsigned long long)hi << 21) ^ (unsigned long long)(lo >> 11);
@@ -2826,22 +2842,29 @@ __global__ __launch_bounds__(256) void verify_normalize_kernel(unsigned long lon
         const Philox q = philox4x32_10<false>((uint32_t)i, (uint32_t)(i >> 32), 0x6e6f726du, 1u, (uint32_t)seed,
                                               (uint32_t)(seed >> 32));
         V3 a = v3(vn_comp(p.w0, p.w1), vn_comp(p.w2, p.w3), vn_comp(q.w0, q.w1));
-        const uint32_t cls = q.w2 & 3u;
-        if (cls == 1u) {                                   // n + dir: unit normal plus a unit vector
-            const V3 nn = divs(a, sqrt(dot(a, a)));
-            a = nn + v3(vn_comp(q.w3, p.w0), vn_comp(p.w1 ^ q.w3, p.w2), vn_comp(p.w3, q.w0 ^ p.w1));
-        } else if (cls == 2u) {                            // one scale for the vector
-            const int e = (int)(q.w3 % 800u) - 400;
-            a = v3(ldexp(a.x, e), ldexp(a.y, e), ldexp(a.z, e));
-        } else if (cls == 3u) {                            // a scale per component
-            a = v3(ldexp(a.x, (int)(q.w3 % 900u) - 450), ldexp(a.y, (int)((q.w3 >> 10) % 900u) - 450),
-                   ldexp(a.z, (int)((q.w3 >> 20) % 900u) - 450));
+        const uint32_t cls = q.w2 & 7u;
+        V3 got;
+        if (cls >= 4u) {                            // the sampler's unit vectors
+            a = sampler_vec(unit31(p.w0 >> 1), unit31(p.w1 >> 1));
+            fp = true;
+            got = normalize_unit(a);
+        } else {
+            if (cls == 1u) {                               // n + dir: unit normal plus a unit vector
+                const V3 nn = divs(a, sqrt(dot(a, a)));
+                a = nn + v3(vn_comp(q.w3, p.w0), vn_comp(p.w1 ^ q.w3, p.w2), vn_comp(p.w3, q.w0 ^ p.w1));
+            } else if (cls == 2u) {                        // one scale for the vector
+                const int e = (int)(q.w3 % 800u) - 400;
+                a = v3(ldexp(a.x, e), ldexp(a.y, e), ldexp(a.z, e));
+            } else if (cls == 3u) {                        // a scale per component
+                a = v3(ldexp(a.x, (int)(q.w3 % 900u) - 450), ldexp(a.y, (int)((q.w3 >> 10) % 900u) - 450),
+                       ldexp(a.z, (int)((q.w3 >> 20) % 900u) - 450));
+            }
+            const double n2 = dot(a, a);
+            const double mn = fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
+            fp = n2 >= 0x1p-760 && n2 <= 0x1p760 && mn >= 0x1p-900;
+            got = normalize(a);
         }
-        const double n2 = dot(a, a);
-        const double mn = fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
-        fp = n2 >= 0x1p-760 && n2 <= 0x1p760 && mn >= 0x1p-900;
-        const V3 got = normalize(a);
-        const V3 want = divs(a, sqrt(n2));
+        const V3 want = divs(a, sqrt(dot(a, a)));
         bad = __double_as_longlong(got.x) != __double_as_longlong(want.x) ||
               __double_as_longlong(got.y) != __double_as_longlong(want.y) ||
               __double_as_longlong(got.z) != __double_as_longlong(want.z);
