@@ -88,7 +88,7 @@ def run(name, spp_scale, dev, stream):
             "full_frame_s_at_config_spp": round(W * H * full_spp / (rate * 1e6), 2),
             "config_gpus": gpus,
             "full_frame_s_on_config_gpus_linear": round(W * H * full_spp / (rate * 1e6) / gpus, 2),
-            "events_per_sample": {k: round(cnt[i] / max(cnt[0], 1), 3) for i, k in enumerate(tipe_rt.COUNTER_NAMES)}}
+            "events_per_sample": {k: round(cnt[i] / max(cnt[0], 1), 7) for i, k in enumerate(tipe_rt.COUNTER_NAMES)}}
 
 
 def main():
