@@ -344,7 +344,7 @@ __device__ __forceinline__ int spheres_exact_scan(const KParams& kp, const V3 o,
 // a strictly smaller t_ref (the reference keeps the first of equal t).
 // Non-finite o, d or Hs^2 > 2^1000 make the ray ambiguous up front.
 // CU (main_cuda.cu's thresholds): t1 >= 0, t2 >= 0.001, one interval pair each.
-template <bool COUNT, bool CU>
+template <bool COUNT, bool CU, bool AMGM = false>
 __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, const V3 d, double a, double two_a,
                                                double four_a, bool fast, double rc2a, double& t_best, Cnt& cnt)
 {
@@ -354,8 +354,14 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     const double aoo = a * fma(o.z, o.z, fma(o.y, o.y, o.x * o.x));
     const double m2a = -2.0 * a;
     const double oax = m2a * o.x, oay = m2a * o.y, oaz = m2a * o.z;
-    // Hs >= (|o| + L) sqrt(a): |o|_1 >= |o|_2; v_rsq_f64 is within 2^-24
-    const double sqa = (a * __builtin_amdgcn_rsq(a)) * (1.0 + 0x1p-20);
+    // Hs >= (|o| + L) sqrt(a): |o|_1 >= |o|_2.  AMGM (the sphere/brute-force
+    // queue kernels without AO or sky): sqrt(a) <= (1 + a)/2, equal at a = 1 (the unit directions
+    // of camera, bounce and AO rays; shorter lerped directions get a looser bound,
+    // more rescans: 1.7e-4 per sample on C2), with 2^-50 for the fma's rounding
+    // for every a >= 0 -- C2 +0.35 %; elsewhere v_rsq_f64 (within 2^-24), which
+    // the BVH instantiations keep (their register allocation lost 1.9 % on C4
+    // with the fma)
+    const double sqa = AMGM ? fma(a, 0.5, 0.5 + 0x1p-50) : (a * __builtin_amdgcn_rsq(a)) * (1.0 + 0x1p-20);
     const double Hs = ((fabs(o.x) + fabs(o.y)) + fabs(o.z) + kp.cand_lmax) * sqa;
     const double Hs2 = Hs * Hs;
     const double T1 = Hs2 * RT_CAND_T1, nT2 = Hs2 * -0x1p-44;
@@ -676,7 +682,7 @@ __device__ __forceinline__ bool cuda_bbox(const KParams& kp, const V3 o, const V
 
 // The sphere half of closest_hit (and the cast counters): the winner index
 // or -1, its t in best (+inf when none).
-template <bool COUNT, bool CU>
+template <bool COUNT, bool CU, bool AMGM = false>
 __device__ __forceinline__ int cast_spheres(const KParams& kp, const V3 o, const V3 d, double& best, Cnt& cnt)
 {
     const double a = dot(d, d);          // sphere.h:20 (same for every sphere)
@@ -690,11 +696,11 @@ __device__ __forceinline__ int cast_spheres(const KParams& kp, const V3 o, const
         cnt.c[RT_CNT_TRI_TESTS] += (unsigned long long)kp.nt;
         wave_slots(cnt, RT_CNT_CAST_LANE_SLOTS);
     }
-    int win = spheres_closest<COUNT, CU>(kp, o, d, a, two_a, four_a, fast, rc2a, best, cnt);
+    int win = spheres_closest<COUNT, CU, AMGM>(kp, o, d, a, two_a, four_a, fast, rc2a, best, cnt);
 #ifdef RT_DUP_SPHERES
     {
         double b2;
-        const int w2 = spheres_closest<COUNT, CU>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, a, two_a,
+        const int w2 = spheres_closest<COUNT, CU, AMGM>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, a, two_a,
                                                   four_a, fast, rc2a, b2, cnt);
         const bool f = opaque_false();
         best = f ? b2 : best;
@@ -704,12 +710,12 @@ __device__ __forceinline__ int cast_spheres(const KParams& kp, const V3 o, const
     return win;
 }
 
-template <bool COUNT, bool BVH, bool CU = false>
+template <bool COUNT, bool BVH, bool CU = false, bool AMGM = false>
 __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const V3 d, double& t_best, int& idx,
                                            Cnt& cnt)
 {
     double best;
-    int win = cast_spheres<COUNT, CU>(kp, o, d, best, cnt);
+    int win = cast_spheres<COUNT, CU, AMGM>(kp, o, d, best, cnt);
     int kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
     int win_orig = 0;
     if (CU && kp.nt > 0 && !cuda_bbox(kp, o, d)) {
@@ -2240,7 +2246,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
             }
         } else if (L.state == SM_CAST) {
             Cnt cnt;
-            L.kind = closest_hit<false, false>(kp, L.o, L.cast_dir(), L.best, L.win, cnt);
+            L.kind = closest_hit<false, false, false, !SKY && AOM != AO_ON>(kp, L.o, L.cast_dir(), L.best, L.win, cnt);
             L.state = SM_RESOLVE;
         }
         QT(8)
