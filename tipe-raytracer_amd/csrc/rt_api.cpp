@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rt/rt.h"
@@ -424,6 +425,7 @@ struct PooledStream {
     hipStream_t st = nullptr;
     void* host = nullptr;            // pinned staging for the D2H copy
     size_t host_bytes = 0;
+    hipEvent_t plane_done[3] = {nullptr, nullptr, nullptr};   // D2H of each output plane
     hipError_t reserve_host(size_t n)
     {
         if (n <= host_bytes) return hipSuccess;
@@ -453,8 +455,12 @@ int stream_pool_get(int device, PooledStream** out)
     DeviceGuard g(device);
     PooledStream* ps = new PooledStream();
     ps->device = device;
-    const hipError_t e = hipStreamCreateWithFlags(&ps->st, hipStreamNonBlocking);
+    hipError_t e = hipStreamCreateWithFlags(&ps->st, hipStreamNonBlocking);
+    for (int i = 0; i < 3 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ps->plane_done[i], hipEventDisableTiming);
     if (e != hipSuccess) {
+        for (hipEvent_t ev : ps->plane_done)
+            if (ev) (void)hipEventDestroy(ev);
+        if (ps->st) (void)hipStreamDestroy(ps->st);
         delete ps;
         return fail(RT_EDEVICE, "device %d stream: %s", device, hipGetErrorString(e));
     }
@@ -482,9 +488,30 @@ void stream_pool_clear()
         DeviceGuard g(ps->device);
         (void)hipStreamSynchronize(ps->st);
         (void)hipStreamDestroy(ps->st);
+        for (hipEvent_t ev : ps->plane_done)
+            if (ev) (void)hipEventDestroy(ev);
         if (ps->host) (void)hipHostFree(ps->host);
         delete ps;
     }
+}
+
+// fn(i0, i1) over [0, n) split into nthr contiguous ranges, the first on
+// the calling thread (host-side scatter of a frame's rows)
+std::atomic<int> g_calls_in_flight{0};    // rt_render_rows calls running (rt_fill_canva's threads)
+
+template <class F>
+void par_ranges(int n, int nthr, const F& fn)
+{
+    nthr = std::max(1, std::min(nthr, n));
+    if (nthr == 1) {
+        fn(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve((size_t)nthr - 1);
+    for (int t = 1; t < nthr; ++t) th.emplace_back(fn, (int)((long long)n * t / nthr), (int)((long long)n * (t + 1) / nthr));
+    fn(0, (int)((long long)n / nthr));
+    for (auto& x : th) x.join();
 }
 
 // Exact bytes of everything rt_scene_upload reads.
@@ -915,6 +942,10 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, i
     const int W = params->largeur_image;
     const int nrows = row_hi - row_lo + 1;
     const int ndev = (int)devs.size();
+    struct InFlight {
+        InFlight() { ++g_calls_in_flight; }
+        ~InFlight() { --g_calls_in_flight; }
+    } in_flight;
     // One device: one band.  Several: cyclic 1-row tiles (load balance: the
     // busiest device renders at most one row more than the average).
     const int k = ndev == 1 ? nrows : 1;
@@ -979,7 +1010,8 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, i
         }
     }
     // 2. every device: D2H of the requested planes into its stream's pinned
-    //    staging buffer, all enqueued before any wait (the copies overlap)
+    //    staging buffer, one copy and event per plane, all enqueued before
+    //    any wait (the devices' copies overlap)
     for (int q = 0; q < ndev; ++q) {
         Slot& s = slots[(size_t)q];
         if (s.n_tiles == 0) continue;
@@ -987,37 +1019,56 @@ int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, i
         size_t nbuf = 0;
         for (int pl = 0; pl < nplanes; ++pl) nbuf += outs[pl] ? s.plane : 0;
         hipError_t e = s.ps->reserve_host(nbuf * sizeof(double));
-        if (e == hipSuccess) e = hipMemcpyAsync(s.ps->host, s.buf, nbuf * sizeof(double), hipMemcpyDeviceToHost, s.ps->st);
+        size_t off = 0;
+        for (int pl = 0; pl < nplanes && e == hipSuccess; ++pl) {
+            if (!outs[pl]) continue;
+            e = hipMemcpyAsync((double*)s.ps->host + off, s.buf + off, s.plane * sizeof(double), hipMemcpyDeviceToHost,
+                               s.ps->st);
+            if (e == hipSuccess) e = hipEventRecord(s.ps->plane_done[pl], s.ps->st);
+            off += s.plane;
+        }
         if (e != hipSuccess) {
             cleanup();
             return fail(RT_EDEVICE, "device %d copy: %s", devs[(size_t)q], hipGetErrorString(e));
         }
     }
-    // 3. wait for each device in turn and scatter its rows into the caller's arrays
+    // 3. each device and plane as its copy lands: scatter its rows into the
+    //    caller's array on several host threads (the next plane is still in
+    //    flight meanwhile)
+    // (concurrent calls, e.g. rt_fill_canva's pthreads, share the threads)
+    const int nthr = std::max(1, std::min(8, (int)std::thread::hardware_concurrency() / 2) / g_calls_in_flight.load());
     for (int q = 0; q < ndev; ++q) {
         Slot& s = slots[(size_t)q];
         if (s.n_tiles == 0) continue;
         DeviceGuard g(devs[(size_t)q]);
-        const hipError_t e = hipStreamSynchronize(s.ps->st);
-        if (e != hipSuccess) {
-            cleanup();
-            return fail(RT_EDEVICE, "device %d render/copy: %s", devs[(size_t)q], hipGetErrorString(e));
-        }
         const double* src0 = (const double*)s.ps->host;
         for (int pl = 0; pl < nplanes; ++pl) {
             if (!outs[pl]) continue;
-            if (ndev == 1) {       // one band: rows row_lo..row_hi are contiguous in both
-                std::memcpy(outs[pl] + (size_t)row_lo * W, src0, sizeof(double) * 3 * (size_t)W * nrows);
-            } else {
-                for (int lt = 0; lt < s.n_tiles; ++lt) {
-                    const int t = q + lt * ndev;
-                    for (int y = 0; y < k; ++y) {
-                        const int gr = row_lo + t * k + y;
-                        if (gr > row_hi) break;
-                        std::memcpy(outs[pl] + (size_t)gr * W, src0 + ((size_t)lt * k + y) * W * 3,
-                                    sizeof(double) * 3 * W);
-                    }
+            const hipError_t e = hipEventSynchronize(s.ps->plane_done[pl]);
+            if (e != hipSuccess) {
+                cleanup();
+                return fail(RT_EDEVICE, "device %d render/copy: %s", devs[(size_t)q], hipGetErrorString(e));
+            }
+            // tile lt of this device = caller rows row_lo + (q + lt * ndev) * k + [0, k)
+            auto scatter = [&, src0, pl](int lt0, int lt1) {
+                for (int lt = lt0; lt < lt1; ++lt) {
+                    const int gr0 = row_lo + (q + lt * ndev) * k;
+                    const int nr = std::min(k, row_hi + 1 - gr0);
+                    if (nr > 0)
+                        std::memcpy(outs[pl] + (size_t)gr0 * W, src0 + (size_t)lt * k * W * 3,
+                                    sizeof(double) * 3 * (size_t)W * nr);
                 }
+            };
+            if (ndev == 1) {       // one band: split its rows instead of its single tile
+                const double* src = src0;
+                auto rows = [&, src, pl](int r0, int r1) {
+                    if (r1 > r0)
+                        std::memcpy(outs[pl] + (size_t)(row_lo + r0) * W, src + (size_t)r0 * W * 3,
+                                    sizeof(double) * 3 * (size_t)W * (r1 - r0));
+                };
+                par_ranges(nrows, nrows * (size_t)W * 24 >= (4u << 20) ? nthr : 1, rows);
+            } else {
+                par_ranges(s.n_tiles, (size_t)s.n_tiles * k * W * 24 >= (4u << 20) ? nthr : 1, scatter);
             }
             src0 += s.plane;
         }
