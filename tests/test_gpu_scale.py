@@ -183,6 +183,31 @@ def test_render_rows_two_device_slots(planes):
         tipe_rt.check(lib.rt_init(0, None))
 
 
+@pytest.mark.parametrize("ndev", [1, 2])
+def test_render_rows_large_band_threaded_scatter(ndev):
+    """Planes of >= 4 MB are scattered into the caller's arrays on several
+    host threads as each plane's D2H copy lands (rt_render_rows step 3):
+    a 1024-wide band of 686 rows on one slot, and cyclic 1-row tiles over two
+    slots, bit-exact against the oracle, rows outside the band untouched."""
+    lib = tipe_rt.lib()
+    devs = (C.c_int * 2)(0, 0)
+    tipe_rt.check(lib.rt_init(ndev, devs))
+    try:
+        bundle = helpers.cornell()
+        W, H, lo, hi = 1024, 700, 5, 690
+        p = helpers.params(W, H, 2, 4, chunks=2)
+        ref = helpers.oracle_render(bundle, p, row_hi=hi, row_lo=lo, nthreads=ORACLE_THREADS)
+        planes = [np.full((H, W, 3), -5.0) for _ in range(3)]
+        tipe_rt.check(lib.rt_render_rows(C.byref(bundle.scene), C.byref(p), hi, lo,
+                                         *[a.ctypes.data for a in planes]))
+        for a, key in zip(planes, ("canva", "albedo", "normal")):
+            assert (a[lo:hi + 1] == ref[key][lo:hi + 1]).all(), key
+            assert (a[:lo] == -5.0).all() and (a[hi + 1:] == -5.0).all(), key
+    finally:
+        lib.rt_shutdown()
+        tipe_rt.check(lib.rt_init(0, None))
+
+
 def test_fill_canva_twelve_threads_auto_chunks():
     """main.c's flow: NUM_THREADS = 12 pthreads call the drop-in on their
     row bands (main.c:407-449: H / 12 rows each, the last one takes the
