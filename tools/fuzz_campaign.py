@@ -1,0 +1,79 @@
+"""GPU-vs-oracle fuzz campaign on seeds the test suite does not use: the four
+families of tests/test_gpu_fuzz.py (random scenes; exact-zero colours on the
+queue kernel; CUDA semantics; 100-400 triangle BVH scenes on a 1-3 block
+queue grid), bit for bit (check_parity: canva, albedo, normal, radiance).
+Prints one line per scene; writes a JSON summary.
+Usage: python3 tools/fuzz_campaign.py OUT.json [scenes per family] [first seed]"""
+import json
+import os
+import sys
+import time
+import traceback
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "tipe-raytracer_amd"))
+
+import tipe_rt  # noqa: E402
+from tipe_rt import scenes  # noqa: E402
+from test_gpu_fuzz import random_scene  # noqa: E402
+from test_gpu_parity import check_parity  # noqa: E402
+
+
+def family_cases(name, seed):
+    if name == "random":
+        return random_scene(seed), None
+    if name == "zero_throughput_queue":
+        return random_scene(seed, zeros=True, chunks=2 + seed % 3), None
+    if name == "cuda_semantics":
+        bundle, p = random_scene(seed)
+        if bundle.mesh is not None:
+            scenes.with_cuda_materials(bundle.mesh)
+        p.semantics = tipe_rt.types.RT_SEM_CUDA
+        return (bundle, p), None
+    if name == "bvh_queue_tiny_grid":
+        bundle, p = random_scene(seed, zeros=bool(seed % 2), chunks=5 + seed % 2, nt_range=(100, 400),
+                                 spp=40 + 8 * (seed % 2))
+        p.largeur_image, p.hauteur_image = min(p.largeur_image, 20), min(p.hauteur_image, 15)
+        return (bundle, p), str(1 + seed % 3)
+    raise ValueError(name)
+
+
+def main():
+    out = sys.argv[1]
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+    first = int(sys.argv[3]) if len(sys.argv) > 3 else 10000
+    fams = ["random", "zero_throughput_queue", "cuda_semantics", "bvh_queue_tiny_grid"]
+    res = {"families": {}, "first_seed": first, "scenes_per_family": n, "failures": []}
+    t0 = time.time()
+    for fi, fam in enumerate(fams):
+        ok = 0
+        for i in range(n):
+            seed = first + fi * 100000 + i
+            (bundle, p), blocks = family_cases(fam, seed)
+            if blocks is None:
+                os.environ.pop("RT_QUEUE_BLOCKS", None)
+            else:
+                os.environ["RT_QUEUE_BLOCKS"] = blocks
+            try:
+                check_parity(bundle, p)
+                ok += 1
+                status = "ok"
+            except AssertionError as e:
+                status = "MISMATCH"
+                res["failures"].append({"family": fam, "seed": seed, "error": str(e)[:400]})
+            except Exception:
+                status = "ERROR"
+                res["failures"].append({"family": fam, "seed": seed, "error": traceback.format_exc()[-400:]})
+            print("%s seed %d %dx%d spp %d B %d chunks %d: %s (%.0f s)" % (
+                fam, seed, p.largeur_image, p.hauteur_image, p.nbRayonParPixel, p.nbRebondMax, p.spp_chunks,
+                status, time.time() - t0), flush=True)
+        res["families"][fam] = {"scenes": n, "bit_exact": ok}
+    os.environ.pop("RT_QUEUE_BLOCKS", None)
+    res["seconds"] = round(time.time() - t0, 1)
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "failures"}), "failures:", len(res["failures"]))
+
+
+if __name__ == "__main__":
+    main()
