@@ -2676,7 +2676,7 @@ static unsigned queue_grid(bool sky, bool ao, int qb)
         if (qb == 0) queue_occupancy_v<0>(sky, ao, nb);
         else if (qb == 3) queue_occupancy_v<3>(sky, ao, nb);
         else queue_occupancy_v<4>(sky, ao, nb);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         c = std::max(1, nb) * std::max(1, ncu);
         if (std::getenv("RT_QUEUE_VERBOSE")) std::fprintf(stderr, "render_kernel_q: %d blocks/CU x %d CUs -> %d\n", nb, ncu, c);
         slot.store(c, std::memory_order_relaxed);
