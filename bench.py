@@ -229,6 +229,39 @@ def configs_extra(dev, stream, cam):
     return out
 
 
+def fp32_extra(dev, stream, cam, spheres):
+    """rt_params.precision = RT_PREC_FP32 (not bit-exact; tests/test_fp32_mode.py
+    bounds its difference from fp64): kernel rates of C2 and C4 at reduced spp,
+    for comparison with the fp64 headline -- never `value`."""
+    out = {}
+    sptr = stream.cuda_stream
+    cases = {"C2": (tipe_rt.make_scene(spheres), 100, 6, False), "C4": (config_scene("tree")[0], 32, 8, True)}
+    for name, (sc, spp, bounces, ao) in cases.items():
+        w, h = 1200, 900
+        p = tipe_rt.make_params(w, h, spp, bounces, cam, focus=3.0, use_ao=ao, ao=2.5, seed=SEED,
+                                chunks=tipe_rt.RT_SPP_CHUNKS_AUTO, precision=tipe_rt.types.RT_PREC_FP32)
+        ds = tipe_rt.DeviceScene(sc, dev.index)
+        tiling = tipe_rt.band_tiling(0, h - 1)
+        buf = torch.empty((3, h, w, 3), dtype=torch.float64, device=dev)
+
+        def launch():
+            tipe_rt.render_async(ds, p, tiling, buf[0].data_ptr(), buf[1].data_ptr(), buf[2].data_ptr(), None, sptr)
+        launch()
+        torch.cuda.synchronize(dev)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(stream)
+        for _ in range(2):
+            launch()
+        ev[1].record(stream)
+        torch.cuda.synchronize(dev)
+        ms = ev[0].elapsed_time(ev[1]) / 2
+        ds.close()
+        out[name] = {"kernel_msamples_per_s": round(w * h * spp / (ms * 1e-3) / 1e6, 1), "spp_measured": spp,
+                     "kernel_ms": round(ms, 3), "dtype": "f32"}
+    out["note"] = "RT_PREC_FP32: same integrator and draws in binary32, sums fp64; not bit-exact (tolerance tests)"
+    return out
+
+
 # ---- end-to-end host-buffer rates of the drop-ins (N = 1) --------------------
 def end_to_end(scene, spheres, cam, reps=2):
     """Upload -> render -> assembled host framebuffer through the C-ABI:
@@ -490,6 +523,7 @@ def main():
         if world == 1 and not args.no_extras:
             rec["configs"] = configs_extra(dev, stream, cam)
             rec["end_to_end"] = end_to_end(scene, spheres, cam)
+            rec["fp32_mode"] = fp32_extra(dev, stream, cam, spheres)
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(scene, cam, threads=args.cpu_threads)
             rec["speedup_vs_cpu_baseline"] = round(value / rec["cpu_baseline"]["value"], 1)

@@ -86,6 +86,7 @@ typedef struct rt_params {
     int accel;                         /* RT_ACCEL_*: triangle traversal          */
     int sky_mode;                      /* RT_SKY_*                                */
     int semantics;                     /* RT_SEM_*: whose integrator               */
+    int precision;                     /* RT_PREC_*: arithmetic of the integrator  */
 } rt_params;
 
 /* rt_params.semantics.  MAIN_C (default) is main.c, the authoritative CPU
@@ -115,6 +116,17 @@ typedef struct rt_params {
  * closest_hit is commented out, main.c:64-71).  LAST_SPHERE enables that
  * branch: when the last sphere is the closest hit, its emissionColor becomes
  * the sky texel sphere_uvmapping (texture.h:92-112) picks and its alpha 1. */
+/* rt_params.precision.  FP64 (default) is the reference's arithmetic, in its
+ * operation order: images equal the CPU oracle's bit for bit.  FP32 runs the
+ * same integrator (main.c semantics, same Philox draws and draw order) in
+ * binary32 -- ray/sphere (stable roots), ray/triangle, sampler, shading --
+ * with the per-pixel sums and the resolve kept in fp64.  It is NOT bit-exact:
+ * paths whose float decisions differ diverge.  The GPU tests bound its
+ * difference from FP64 (tests/test_fp32_mode.py).  FP32 needs
+ * RT_SEM_MAIN_C; it runs the fixed-grid kernel. */
+#define RT_PREC_FP64 0
+#define RT_PREC_FP32 1
+
 #define RT_SKY_OFF 0
 #define RT_SKY_LAST_SPHERE 1
 

@@ -783,6 +783,7 @@ static int validate(const rt_scene* sc, const rt_params* p)
     if (p->rng != RT_RNG_GLIBC && p->rng != RT_RNG_PHILOX) return RT_EINVAL;
     if (p->semantics != RT_SEM_MAIN_C && p->semantics != RT_SEM_CUDA) return RT_EINVAL;
     if (p->semantics == RT_SEM_CUDA && p->sky_mode != RT_SKY_OFF) return RT_EINVAL;
+    if (p->precision != RT_PREC_FP64) return RT_EINVAL;   /* the restatement is the fp64 spec only */
     if (sc->nbSpheres < 0 || sc->nbTriangles < 0) return RT_EINVAL;
     if (sc->nbSpheres > 0 && !sc->sphere_list) return RT_EINVAL;
     if (sc->nbTriangles > 0) {

@@ -61,7 +61,7 @@ int main(void) {
   O(rt_material, alpha); O(rt_triangle, uvB); O(rt_thread_data, nbRayonParPixel);
   O(rt_thread_data, triangle_list); O(rt_thread_data, AO_intensity); O(rt_scene, quelMatPourTri);
   O(rt_params, cam); O(rt_params, focus_distance); O(rt_params, rng); O(rt_params, spp_chunks);
-  O(rt_params, seed); O(rt_frame, radiance);
+  O(rt_params, seed); O(rt_params, semantics); O(rt_params, precision); O(rt_frame, radiance);
   return 0;
 }
 """

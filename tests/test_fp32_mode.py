@@ -1,0 +1,94 @@
+"""rt_params.precision = RT_PREC_FP32 (rt.h): the integrator in binary32.
+
+This mode is NOT bit-exact.  It makes the same Philox draws in the same order
+as the fp64 path, so most paths follow the fp64 path up to float rounding, and
+a path diverges only where a float decision (hit/miss, nearest surface,
+refraction draw against alpha) comes out differently.  The bar here is the
+fp64 image from the bit-exact kernel, which the parity suite pins to the
+oracle.  The tolerances, measured on the same scenes:
+  * per-channel image means of pre-gamma radiance within REL_MEAN (relative);
+  * per-pixel mean absolute radiance difference within REL_MAE of the mean;
+  * at most CANVA_FRAC of the 8-bit canva values more than CANVA_LEVELS apart.
+The fp64 oracle refuses precision FP32 (it restates fp64 only).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import helpers
+import tipe_rt
+from tipe_rt import types as T
+
+REL_MEAN = 0.03
+REL_MAE = 0.06
+CANVA_LEVELS = 16
+CANVA_FRAC = 0.06
+
+
+def test_precision_validation_without_device():
+    L = tipe_rt.lib()
+    sc = T.Scene()
+    p = T.Params()
+    L.rt_params_init(C.byref(p))
+    assert p.precision == T.RT_PREC_FP64
+    p.largeur_image, p.hauteur_image, p.nbRayonParPixel, p.nbRebondMax = 8, 6, 1, 5
+    buf = (C.c_double * (8 * 6 * 3))()
+    p.precision = 7
+    assert L.rt_render_rows(C.byref(sc), C.byref(p), 5, 0, buf, None, None) == T.RT_EINVAL
+    p.precision, p.semantics = T.RT_PREC_FP32, T.RT_SEM_CUDA
+    assert L.rt_render_rows(C.byref(sc), C.byref(p), 5, 0, buf, None, None) == T.RT_EUNSUPPORTED
+
+
+def test_oracle_refuses_fp32():
+    p = helpers.params(8, 6, 1, 2)
+    p.precision = T.RT_PREC_FP32
+    with pytest.raises(AssertionError):
+        helpers.oracle_render(helpers.cornell(), p)
+
+
+def _gpu_render(bundle, p):
+    from test_gpu_parity import gpu_render
+    return gpu_render(bundle, p)
+
+
+def _mineways():
+    tris, qm, mats, tw, th, nm = tipe_rt.scenes.load_mesh_fixture("mineways")
+    for t in tris:
+        for P in (t.A, t.B, t.C):
+            P.e[0] = P.e[0] * 0.1 - 0.2
+            P.e[1] = P.e[1] * 0.1 - 1.0
+            P.e[2] = P.e[2] * 0.1 - 2.5
+    return helpers.SceneBundle(tipe_rt.scenes.cornell_spheres(), (tris, qm, mats, tw, th, nm))
+
+
+CASES = {
+    "cornell": lambda: (helpers.cornell(), helpers.params(96, 72, 64, 6, chunks=4)),
+    "cornell_ao": lambda: (helpers.cornell(), helpers.params(64, 48, 32, 6, use_ao=True)),
+    "pyramid": lambda: (helpers.pyramid_scene(), helpers.params(64, 48, 32, 6)),
+    "mineways": lambda: (_mineways(), helpers.params(48, 36, 16, 6)),
+    "tree_ao": lambda: (helpers.tree_scene(), helpers.params(48, 36, 16, 8, use_ao=True)),
+    "sky": lambda: (helpers.sky_scene(), helpers.params(48, 36, 16, 5, sky_mode=1)),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_fp32_close_to_fp64(name):
+    bundle, p = CASES[name]()
+    c64, _, _, r64 = _gpu_render(bundle, p)
+    p.precision = T.RT_PREC_FP32
+    c32, a32, n32, r32 = _gpu_render(bundle, p)
+    for b in (c32, a32, n32, r32):
+        assert (b != -1.0).any(), "fp32 kernel wrote nothing"
+    r64, r32 = np.nan_to_num(r64), np.nan_to_num(r32)
+    m64 = r64.reshape(-1, 3).mean(0)
+    m32 = r32.reshape(-1, 3).mean(0)
+    mae = np.abs(r32 - r64).reshape(-1, 3).mean(0)
+    far = float((np.abs(c32 - c64) > CANVA_LEVELS).mean())
+    scale = np.maximum(m64, 1e-3)
+    print("fp32 %s: rel mean %s, rel mae %s, canva far %.5f, identical canva %.4f" %
+          (name, np.round(np.abs(m32 - m64) / scale, 5), np.round(mae / scale, 5), far, float((c32 == c64).mean())))
+    assert (np.abs(m32 - m64) <= REL_MEAN * scale).all()
+    assert (mae <= REL_MAE * scale).all()
+    assert far <= CANVA_FRAC

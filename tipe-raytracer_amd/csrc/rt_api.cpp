@@ -104,6 +104,10 @@ int validate_params(const rt_params* p)
         return fail(RT_EINVAL, "unknown semantics %d", p->semantics);
     if (p->semantics == RT_SEM_CUDA && p->sky_mode != RT_SKY_OFF)
         return fail(RT_EINVAL, "sky_mode needs RT_SEM_MAIN_C (main_cuda.cu has no sky)");
+    if (p->precision != RT_PREC_FP64 && p->precision != RT_PREC_FP32)
+        return fail(RT_EINVAL, "unknown precision %d", p->precision);
+    if (p->precision == RT_PREC_FP32 && p->semantics != RT_SEM_MAIN_C)
+        return fail(RT_EUNSUPPORTED, "RT_PREC_FP32 needs RT_SEM_MAIN_C");
     if ((unsigned long long)p->largeur_image * (unsigned long long)p->hauteur_image > 0xffffffffull)
         return fail(RT_EUNSUPPORTED, "pixel index exceeds the 32-bit Philox counter word");
     return RT_OK;
@@ -268,6 +272,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.sph_disp = sc->sph_disp;
     kp.tri_mat = sc->tri_mat;
     kp.cuda = p->semantics == RT_SEM_CUDA ? 1 : 0;
+    kp.f32 = p->precision == RT_PREC_FP32 ? 1 : 0;
     for (int i = 0; i < 6; ++i) kp.cbb[i] = sc->cbb[i];
     if (p->sky_mode == RT_SKY_LAST_SPHERE && sc->sky && sc->ns > 0) {
         kp.sky = sc->sky;

@@ -189,7 +189,8 @@ def make_scene(spheres=None, triangles=None, quel_mat=None, mat_list=None, tex_w
 
 
 def make_params(W, H, spp, bounces, cam, focus=3.0, aperture=(0.0, 0.0), use_ao=False, ao=2.5,
-                seed=1010, rng=RT_RNG_PHILOX, compat=1, chunks=1, accel=0, sky_mode=0, semantics=0):
+                seed=1010, rng=RT_RNG_PHILOX, compat=1, chunks=1, accel=0, sky_mode=0, semantics=0,
+                precision=0):
     p = Params()
     p.largeur_image, p.hauteur_image = W, H
     p.nbRayonParPixel, p.nbRebondMax = spp, bounces
@@ -203,6 +204,7 @@ def make_params(W, H, spp, bounces, cam, focus=3.0, aperture=(0.0, 0.0), use_ao=
     p.accel = accel
     p.sky_mode = sky_mode
     p.semantics = semantics
+    p.precision = precision
     return p
 
 
