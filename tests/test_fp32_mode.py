@@ -5,7 +5,9 @@ as the fp64 path, so most paths follow the fp64 path up to float rounding, and
 a path diverges only where a float decision (hit/miss, nearest surface,
 refraction draw against alpha) comes out differently.  The bar here is the
 fp64 image from the bit-exact kernel, which the parity suite pins to the
-oracle.  The tolerances, measured on the same scenes:
+oracle.  Measured (r02): image means and per-pixel MAE agree within 1e-3
+(sky scene; 0 to 5e-5 elsewhere), >= 99.5 % of canva values identical, none
+more than 16 levels apart except 0.02 % on the sky scene.  The tolerances:
   * per-channel image means of pre-gamma radiance within REL_MEAN (relative);
   * per-pixel mean absolute radiance difference within REL_MAE of the mean;
   * at most CANVA_FRAC of the 8-bit canva values more than CANVA_LEVELS apart.
@@ -20,10 +22,10 @@ import helpers
 import tipe_rt
 from tipe_rt import types as T
 
-REL_MEAN = 0.03
-REL_MAE = 0.06
+REL_MEAN = 0.005
+REL_MAE = 0.005
 CANVA_LEVELS = 16
-CANVA_FRAC = 0.06
+CANVA_FRAC = 0.002
 
 
 def test_precision_validation_without_device():

@@ -2203,6 +2203,9 @@ __device__ __forceinline__ void trace_f32(const KParams& kp, const F32Scene& fs,
             if (rc.x > 0.5f || rc.y > 0.5f || rc.z > 0.5f) rc = mulv3(diff, mul3(rc, 1.3f));
             rc = mulv3(diff, rc);
         }
+        // zero-throughput exit (host-gated as for fp64, LanePath::zero_rc): the
+        // chain is over and every later bounce adds emis * 0
+        if (kp.zero_exit && rc.x == 0.0f && rc.y == 0.0f && rc.z == 0.0f) break;
     }
     acc_add(acc, ACC_RAD, v3f(inc));
 }
