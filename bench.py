@@ -235,7 +235,7 @@ def fp32_extra(dev, stream, cam, spheres):
     for comparison with the fp64 headline -- never `value`."""
     out = {}
     sptr = stream.cuda_stream
-    cases = {"C2": (tipe_rt.make_scene(spheres), 100, 6, False), "C4": (config_scene("tree")[0], 32, 8, True)}
+    cases = {"C2": (tipe_rt.make_scene(spheres), 1000, 6, False), "C4": (config_scene("tree")[0], 32, 8, True)}
     for name, (sc, spp, bounces, ao) in cases.items():
         w, h = 1200, 900
         p = tipe_rt.make_params(w, h, spp, bounces, cam, focus=3.0, use_ao=ao, ao=2.5, seed=SEED,

@@ -2108,110 +2108,146 @@ __device__ __forceinline__ float ao_f32(const KParams& kp, const F32Scene& fs, F
     return occ / AO;
 }
 
+// The samples [s0, s1) of one pixel as a flat loop of bounces (tracer,
+// main.c:118-242, in float): one iteration is one bounce of the sample in
+// flight, and a lane whose path ends starts its next sample's camera ray in
+// the next iteration, so a wave does not wait for its longest path before
+// any lane moves on (the fp64 kernels' LanePath rounds, in miniature).
 template <bool BVH, bool SKY>
-__device__ __forceinline__ void trace_f32(const KParams& kp, const F32Scene& fs, F3 o, F3 d, Stream& st,
-                                          double* acc)
+__device__ __forceinline__ void samples_f32(const KParams& kp, const F32Scene& fs, int x, int g, uint32_t pixel,
+                                            int s0, int s1, uint32_t* rng, double* acc)
 {
+    if (kp.B <= 0) return;                               // tracer adds (0, 0, 0) everywhere
+    Stream st;
+    F3 o, d, inc, rc;
     bool chain = true;
     float top_n2 = 1.0f;
-    F3 inc = f3(0, 0, 0), rc = f3(1, 1, 1);
-    if (kp.B <= 0) {
-        acc_add(acc, ACC_ALB, v3(0, 0, 0));
-        acc_add(acc, ACC_NRM, v3(0, 0, 0));
-    }
-    for (int i = 0; i < kp.B; i++) {
+    int i = 0, s = s0;
+    st.start(pixel, 0u, kp.key0, kp.key1, rng);          // the keys stay wave-uniform (SGPRs)
+    auto start = [&]() {                                 // the camera ray of sample s (main.c:258-270)
+        st.sample = (uint32_t)(kp.s_base + s);
+        st.n = 0;
+        V3 no, rd;
+        camera_ray<false>(kp, x, g, st, no, rd);
+        o = f3v(no);
+        d = f3v(rd);
+        inc = f3(0, 0, 0);
+        rc = f3(1, 1, 1);
+        chain = true;
+        top_n2 = 1.0f;
+        i = 0;
+    };
+    if (s < s1) start();
+    while (s < s1) {
+        bool end = false, add_inc = true;
         float t;
         int idx;
         const int kind = closest_f32<BVH>(kp, fs, o, d, t, idx);
-        if (kind == HIT_NONE) {
+        if (kind == HIT_NONE) {                          // miss: the path ends, main.c:236-238
             if (chain) {
                 acc_add(acc, ACC_ALB, v3(0, 0, 0));
                 acc_add(acc, ACC_NRM, v3(0, 0, 0));
             }
-            break;
-        }
-        const F3 hp = add3(o, mul3(d, t));
-        F3 hn;
-        Mat mat;
-        if (kind == HIT_SPHERE) {
-            const float4 s = f32_sphere(kp, fs, idx);
-            hn = norm3(sub3(hp, f3(s.x, s.y, s.z)));
-            mat = load_mat(kp.sph_mat + idx);
-            if (SKY && idx == kp.ns - 1) sky_material(kp, idx, kp.sph[idx], v3f(hp), mat);
+            end = true;
         } else {
-            const TriGeo g = kp.tri[idx];
-            const V3 hn64 = normalize(v3(g.nx, g.ny, g.nz));
-            hn = f3v(hn64);
-            mat = tri_material(kp, idx, v3f(hp), hn64);
-        }
-        const float alpha = (float)mat.alpha;
-        if (chain) {
-            if (mat.es > 0) {                            // direct view of a light, main.c:154-160
-                V3 col;
-                if (kind == HIT_SPHERE && !(SKY && idx == kp.ns - 1)) {
-                    const double* sd = kp.sph_disp + 3 * idx;
-                    col = v3(sd[0], sd[1], sd[2]);
-                } else {
-                    col = hsl_roundtrip(mat.emis);
-                }
-                acc_add(acc, ACC_RAD, col);
-                acc_add(acc, ACC_ALB, col);
-                acc_add(acc, ACC_NRM, v3f(hn));
-                return;
-            }
-            if (!(alpha < 0.0001f) || i == kp.B - 1) {
-                acc_add(acc, ACC_ALB, mat.diff);
-                acc_add(acc, ACC_NRM, v3f(hn));
-                chain = alpha < 0.0001f;
-            }
-        }
-        o = hp;
-        const F3 diffuse_dir = norm3(add3(hn, random_dir_f32(st)));
-        const F3 reflected_dir = sub3(d, mul3(hn, 2.0f * dot3(d, hn)));
-        const F3 dr = add3(diffuse_dir, mul3(sub3(reflected_dir, diffuse_dir), (float)mat.rs));
-        if (alpha < 0.0001f) continue;                   // alpha hole, main.c:200-206
-        chain = false;
-        if (alpha <= 0.99f) {                            // refraction, main.c:167-193
-            F3 nn = hn;
-            float n1, n2;
-            const float ior = (float)mat.ior;
-            if (dot3(d, hn) > 0.0f) {
-                nn = f3(-hn.x, -hn.y, -hn.z);
-                n1 = ior;
-                n2 = top_n2;
+            const F3 hp = add3(o, mul3(d, t));
+            F3 hn;
+            Mat mat;
+            if (kind == HIT_SPHERE) {
+                const float4 sg = f32_sphere(kp, fs, idx);
+                hn = norm3(sub3(hp, f3(sg.x, sg.y, sg.z)));
+                mat = load_mat(kp.sph_mat + idx);
+                if (SKY && idx == kp.ns - 1) sky_material(kp, idx, kp.sph[idx], v3f(hp), mat);
             } else {
-                n1 = top_n2;
-                n2 = ior;
-                top_n2 = ior;
+                const TriGeo tg = kp.tri[idx];
+                const V3 hn64 = normalize(v3(tg.nx, tg.ny, tg.nz));
+                hn = f3v(hn64);
+                mat = tri_material(kp, idx, v3f(hp), hn64);
             }
-            const F3 refr = refracted_f32(d, nn, n1, n2);
-            if (unit31f(st.next31()) > alpha) {
-                d = refr;
-                continue;
+            const float alpha = (float)mat.alpha;
+            bool lit = false;
+            if (chain) {
+                if (mat.es > 0) {                        // direct view of a light, main.c:154-160
+                    V3 col;
+                    if (kind == HIT_SPHERE && !(SKY && idx == kp.ns - 1)) {
+                        const double* sd = kp.sph_disp + 3 * idx;
+                        col = v3(sd[0], sd[1], sd[2]);
+                    } else {
+                        col = hsl_roundtrip(mat.emis);
+                    }
+                    acc_add(acc, ACC_RAD, col);
+                    acc_add(acc, ACC_ALB, col);
+                    acc_add(acc, ACC_NRM, v3f(hn));
+                    lit = true;
+                } else if (!(alpha < 0.0001f) || i == kp.B - 1) {
+                    acc_add(acc, ACC_ALB, mat.diff);
+                    acc_add(acc, ACC_NRM, v3f(hn));
+                    chain = alpha < 0.0001f;
+                }
+            }
+            if (lit) {
+                end = true;
+                add_inc = false;
+            } else {
+                o = hp;
+                const F3 diffuse_dir = norm3(add3(hn, random_dir_f32(st)));
+                const F3 reflected_dir = sub3(d, mul3(hn, 2.0f * dot3(d, hn)));
+                const F3 dr = add3(diffuse_dir, mul3(sub3(reflected_dir, diffuse_dir), (float)mat.rs));
+                bool shaded = !(alpha < 0.0001f);            // alpha hole: pass through, main.c:200-206
+                if (shaded) {
+                    chain = false;
+                    if (alpha <= 0.99f) {                    // refraction, main.c:167-193
+                        F3 nn = hn;
+                        float n1, n2;
+                        const float ior = (float)mat.ior;
+                        if (dot3(d, hn) > 0.0f) {
+                            nn = f3(-hn.x, -hn.y, -hn.z);
+                            n1 = ior;
+                            n2 = top_n2;
+                        } else {
+                            n1 = top_n2;
+                            n2 = ior;
+                            top_n2 = ior;
+                        }
+                        const F3 refr = refracted_f32(d, nn, n1, n2);
+                        if (unit31f(st.next31()) > alpha) {
+                            d = refr;
+                            shaded = false;
+                        }
+                    }
+                }
+                if (shaded) {
+                    d = dr;
+                    const F3 diff = f3v(mat.diff), emis = f3v(mat.emis);
+                    if (kp.useAO) {
+                        const float AO = (float)((cdptr)kp.uni)[opq0() + U_AO];
+                        inc = add3(inc, mulv3(mul3(emis, (float)mat.es * 1.5f * AO), rc));
+                        if (rc.x > 0.5f || rc.y > 0.5f || rc.z > 0.5f) rc = mulv3(diff, mul3(rc, 1.3f));
+                        rc = mulv3(diff, rc);
+                        rc = mul3(rc, ao_f32<BVH>(kp, fs, hp, hn, AO, st));
+                    } else {
+                        inc = add3(inc, mulv3(mul3(emis, (float)mat.es), rc));
+                        if (rc.x > 0.5f || rc.y > 0.5f || rc.z > 0.5f) rc = mulv3(diff, mul3(rc, 1.3f));
+                        rc = mulv3(diff, rc);
+                    }
+                    // zero-throughput exit (host-gated as for fp64, LanePath::zero_rc):
+                    // the chain is over and every later bounce adds emis * 0
+                    if (kp.zero_exit && rc.x == 0.0f && rc.y == 0.0f && rc.z == 0.0f) end = true;
+                }                                            // (a hole's ray goes on unchanged)
+                ++i;
+                if (i >= kp.B) end = true;
             }
         }
-        d = dr;
-        const F3 diff = f3v(mat.diff), emis = f3v(mat.emis);
-        if (kp.useAO) {
-            const float AO = (float)((cdptr)kp.uni)[opq0() + U_AO];
-            inc = add3(inc, mulv3(mul3(emis, (float)mat.es * 1.5f * AO), rc));
-            if (rc.x > 0.5f || rc.y > 0.5f || rc.z > 0.5f) rc = mulv3(diff, mul3(rc, 1.3f));
-            rc = mulv3(diff, rc);
-            rc = mul3(rc, ao_f32<BVH>(kp, fs, hp, hn, AO, st));
-        } else {
-            inc = add3(inc, mulv3(mul3(emis, (float)mat.es), rc));
-            if (rc.x > 0.5f || rc.y > 0.5f || rc.z > 0.5f) rc = mulv3(diff, mul3(rc, 1.3f));
-            rc = mulv3(diff, rc);
+        if (end) {
+            if (add_inc) acc_add(acc, ACC_RAD, v3f(inc));
+            ++s;
+            if (s < s1) start();
         }
-        // zero-throughput exit (host-gated as for fp64, LanePath::zero_rc): the
-        // chain is over and every later bounce adds emis * 0
-        if (kp.zero_exit && rc.x == 0.0f && rc.y == 0.0f && rc.z == 0.0f) break;
     }
-    acc_add(acc, ACC_RAD, v3f(inc));
 }
 
 // fill_canva's thread = (pixel, chunk of its samples), as render_body, with
-// trace_f32.  The camera ray is built in fp64 (camera_ray) and rounded.
+// samples_f32.  The camera ray is built in fp64 (camera_ray) and rounded.
 template <bool BVH, bool SKY>
 __global__ __launch_bounds__(256) void render_kernel_f32(const KParams kp)
 {
@@ -2258,13 +2294,7 @@ __global__ __launch_bounds__(256) void render_kernel_f32(const KParams kp)
     const bool carry = kp.sums && kp.chunks == 1;
 #pragma unroll
     for (int j = 0; j < 9; ++j) acc[j * 256] = carry ? kp.sums[li * 9 + j] : 0.0;
-    for (int s = s0; s < s1; ++s) {
-        Stream st;
-        st.start(pixel, (uint32_t)(kp.s_base + s), kp.key0, kp.key1, rng_lds + threadIdx.x);
-        V3 no, rd;
-        camera_ray<false>(kp, x, g, st, no, rd);
-        trace_f32<BVH, SKY>(kp, fs, f3v(no), f3v(rd), st, acc);
-    }
+    samples_f32<BVH, SKY>(kp, fs, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc);
     const V3 srad = v3(acc[0], acc[256], acc[512]);
     const V3 salb = v3(acc[768], acc[1024], acc[1280]);
     const V3 snrm = v3(acc[1536], acc[1792], acc[2048]);
