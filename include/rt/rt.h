@@ -207,6 +207,12 @@ void* rt_fill_canva(void* thread_data);
  * Process-wide; returns the previous setting. */
 int rt_set_fill_spp_chunks(int spp_chunks);
 
+/* The rt_params.precision rt_fill_canva renders with: RT_PREC_FP64 (default,
+ * bit-exact) or RT_PREC_FP32 (the fast mode, not bit-exact; see
+ * rt_params.precision).  Other values select FP64.  Process-wide; returns the
+ * previous setting. */
+int rt_set_fill_precision(int precision);
+
 /* rt_render_rows / rt_fill_canva keep the uploaded scene (and its BVH) of
  * the last few distinct scenes per device, keyed by the exact bytes of the
  * caller's arrays, so the NUM_THREADS calls of one frame upload it once.

@@ -94,3 +94,56 @@ def test_fp32_close_to_fp64(name):
     assert (np.abs(m32 - m64) <= REL_MEAN * scale).all()
     assert (mae <= REL_MAE * scale).all()
     assert far <= CANVA_FRAC
+
+
+def test_fill_precision_setter_round_trip():
+    L = tipe_rt.lib()
+    assert L.rt_set_fill_precision(T.RT_PREC_FP32) == T.RT_PREC_FP64
+    assert L.rt_set_fill_precision(5) == T.RT_PREC_FP32          # invalid selects FP64
+    assert L.rt_set_fill_precision(T.RT_PREC_FP64) == T.RT_PREC_FP64
+
+
+@pytest.mark.gpu
+def test_fill_canva_fp32_close_to_fp64():
+    """main.c's drop-in (rt_fill_canva, 3 pthreads over row bands) with
+    rt_set_fill_precision(RT_PREC_FP32), against the same drop-in in FP64."""
+    import threading
+    from tipe_rt.types import ThreadData, Sphere
+    bundle = helpers.cornell()
+    W, H, S, B = 48, 36, 16, 5
+    p = helpers.params(W, H, S, B)
+    L = tipe_rt.lib()
+
+    def fill():
+        canva = np.zeros((H, W, 3))
+        tds = []
+        for hi, lo in [(35, 24), (23, 12), (11, 0)]:
+            td = ThreadData()
+            td.start_row, td.end_row = hi, lo
+            td.canva = C.cast(canva.ctypes.data, C.POINTER(tipe_rt.Vec3))
+            td.cam = p.cam
+            td.largeur_image, td.hauteur_image = W, H
+            td.nbRayonParPixel, td.nbRebondMax = S, B
+            td.total_pixels = W * H
+            td.sphere_list = C.cast(bundle.spheres, C.POINTER(Sphere))
+            td.nbSpheres = len(bundle.spheres)
+            td.focus_distance = 3
+            tds.append(td)
+        res = []
+        ths = [threading.Thread(target=lambda t=t: res.append(L.rt_fill_canva(C.byref(t)))) for t in tds]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        assert all(r is None for r in res), L.rt_last_error()
+        return canva
+
+    c64 = fill()
+    prev = L.rt_set_fill_precision(T.RT_PREC_FP32)
+    try:
+        c32 = fill()
+    finally:
+        L.rt_set_fill_precision(prev)
+    assert c64.max() > 0
+    assert float((np.abs(c32 - c64) > CANVA_LEVELS).mean()) <= CANVA_FRAC
+    assert abs(c32.mean() - c64.mean()) <= REL_MEAN * c64.mean()

@@ -424,6 +424,7 @@ int launch_on_stream(KParams& kp, const double* uni, hipStream_t st, bool count)
 //  * frame planes are stream-ordered allocations (hipMallocAsync) from the
 //    device pool whose release threshold launch_on_stream raises.
 std::atomic<int> g_fill_chunks{RT_SPP_CHUNKS_AUTO};
+std::atomic<int> g_fill_prec{RT_PREC_FP64};
 
 struct PooledStream {
     int device = 0;
@@ -1093,6 +1094,11 @@ int rt_set_fill_spp_chunks(int spp_chunks)
     if (spp_chunks < RT_SPP_CHUNKS_AUTO) spp_chunks = 1;
     return g_fill_chunks.exchange(spp_chunks);
 }
+int rt_set_fill_precision(int precision)
+{
+    if (precision != RT_PREC_FP32) precision = RT_PREC_FP64;
+    return g_fill_prec.exchange(precision);
+}
 int rt_scene_cache_clear(void) { return scene_cache_clear(); }
 rt_denoise_fn rt_get_denoise_hook(void) { return g_denoise.load(); }
 
@@ -1170,6 +1176,7 @@ void* rt_fill_canva(void* arg)
     p.useAO = d->useAO ? 1 : 0;
     p.compat_int_truncation = 0;
     p.spp_chunks = g_fill_chunks.load();
+    p.precision = g_fill_prec.load();
     const int rc = rt_render_rows(&sc, &p, d->start_row, d->end_row, d->canva, d->albedo_tab, d->normal_tab);
     return rc == RT_OK ? nullptr : (void*)1;
 }

@@ -71,6 +71,8 @@ def lib():
         L.rt_set_zero_throughput_exit.restype = C.c_int
         L.rt_set_fill_spp_chunks.argtypes = [C.c_int]
         L.rt_set_fill_spp_chunks.restype = C.c_int
+        L.rt_set_fill_precision.argtypes = [C.c_int]
+        L.rt_set_fill_precision.restype = C.c_int
         L.rt_scene_cache_clear.restype = C.c_int
         L.rt_denoise_pack.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6
         L.rt_denoise_unpack.argtypes = [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
@@ -84,7 +86,7 @@ EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error",
                     "rt_scene_release", "rt_render_async", "rt_assemble_async", "rt_count_async",
                     "rt_selftest_math", "rt_accumulate_async", "rt_resolve_async", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
                     "rt_denoise_unpack", "rt_denoise_pack_async", "rt_verify_sampler_phi",
-                    "rt_verify_sphere_pass", "rt_verify_normalize", "rt_set_zero_throughput_exit", "rt_set_fill_spp_chunks",
+                    "rt_verify_sphere_pass", "rt_verify_normalize", "rt_set_zero_throughput_exit", "rt_set_fill_spp_chunks", "rt_set_fill_precision",
                     "rt_scene_cache_clear"]
 
 # rt_denoise_fn (rt.h): denoiser()'s signature, denoiser.h:31
