@@ -26,7 +26,11 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+/* 2: rt_params gained `precision` (RT_PREC_*) and rt_params_init defaults
+ *    spp_chunks to RT_SPP_CHUNKS_AUTO (a different summation grouping than
+ *    the strict fill_canva order of spp_chunks = 1); build rt_params with
+ *    rt_params_init so new fields read their defaults.  rt_gather_async.  */
+#define RT_ABI_VERSION 2
 
 /* ---- status codes ------------------------------------------------------- */
 #define RT_OK            0
@@ -257,6 +261,27 @@ int rt_render_async(const rt_device_scene* scene, const rt_params* params,
 int rt_assemble_async(const rt_color* gathered, long long rank_stride, int world,
                       int tile_rows, int rows_per_rank, int W, int H,
                       rt_color* out, void* hip_stream);
+
+/* ---- device-resident multi-device frame ---------------- */
+/* Replaces main_cuda.cu:280-339 (one device, three D2H copies) for a device
+ * destination on several devices of one node.  rt_gather_async copies slot
+ * r's local plane (rows_per_rank*W colours on device src_devices[r], rendered
+ * with tiling {0, tile_rows, r, world, rows_per_rank/tile_rows}) into a
+ * rank-major staging block on dst_device with peer copies (xGMI), then
+ * un-permutes the staging into out (W*H colours on dst_device), all on
+ * hip_stream (a stream of dst_device; the caller orders the slots' renders
+ * before it, e.g. with events).
+ * rt_render_gather_async does the whole frame: every device of rt_init's list
+ * (default: device 0) renders its cyclic tile_rows-row tiles on a pooled
+ * stream of its own (after the work already enqueued on hip_stream), and the
+ * requested planes of `frame` (device pointers on the list's FIRST device,
+ * W*H colours each) are gathered and assembled on hip_stream.  Asynchronous;
+ * images are bit-identical to one device's rt_render_async (the stream is
+ * keyed by the global pixel). */
+int rt_gather_async(int world, const int* src_devices, const rt_color* const* locals, int tile_rows,
+                    int rows_per_rank, int W, int H, int dst_device, rt_color* out, void* hip_stream);
+int rt_render_gather_async(const rt_scene* scene, const rt_params* params, int tile_rows, const rt_frame* frame,
+                           void* hip_stream);
 
 /* ---- instrumentation (roofline accounting, tests) ----------------------- */
 enum {

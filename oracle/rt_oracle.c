@@ -62,6 +62,8 @@ typedef struct ctx {
     int sky;                 /* rt.h RT_SKY_LAST_SPHERE with a sky table */
     int cuda;                /* rt.h RT_SEM_CUDA: main_cuda.cu's integrator */
     rt_point3 bb_lo, bb_hi;  /* CUDA mode: the triangles' bounding box */
+    int mesh_cull;           /* main.c mode: skip the triangle scan for rays that miss mb_lo..mb_hi */
+    rt_point3 mb_lo, mb_hi;  /* the triangles' box padded by 2^-16 (1 + max |coordinate|) */
     uint64_t seed;
     uint32_t pixel, sample, n;
     uint32_t block[4];
@@ -228,9 +230,11 @@ static oracle_hit hit_triangle_eps(ctx* c, const rt_triangle* tri, rt_ray r, dou
     double v = -dot(edgeAB, dao) * invDet;
     double w = 1 - u - v;
     h.didHit = det >= 1E-6 && dst >= eps && u >= eps && v >= eps && w >= eps;
-    h.hitPoint = add(r.origin, mul_s(r.dir, dst));
-    h.normal = normalize(normalVect);
     h.dst = dst;
+    if (h.didHit) {          /* read only for a hit (speed: the same values mesh.h:91-92 computes) */
+        h.hitPoint = add(r.origin, mul_s(r.dir, dst));
+        h.normal = normalize(normalVect);
+    }
     return h;
 }
 
@@ -304,6 +308,38 @@ static rt_material sphere_uvmapping(ctx* c, const rt_sphere* s, rt_vec3 hitPoint
     return sc->sky_mat_list[index];
 }
 
+/* Speed only (test infrastructure, not a reference function): a conservative
+ * test whether the ray can meet the triangles' box mb_lo..mb_hi at t >= 0.
+ * An accepted hit_triangle needs det >= 1e-6 and u, v, w >= 1e-7, so the exact
+ * ray-plane point lies within the triangle up to the rounding of u and v
+ * (first order: a few ulp of the coordinates scaled by 1/det, below 1e-8 for
+ * coordinates of magnitude <= 1e3); the box is padded by 2^-16 (1 + max
+ * |coordinate|), far above that, and the slab distances are widened by
+ * 2^-30 relative.  Non-finite rays always scan.  oracle_set_mesh_cull(0)
+ * turns it off (tests/test_oracle.py checks both give the same frames). */
+static int g_mesh_cull = 1;
+void oracle_set_mesh_cull(int on) { g_mesh_cull = on; }
+static int meets_mesh_box(const ctx* c, rt_ray r)
+{
+    double t0 = 0.0, t1 = INFINITY;
+    for (int k = 0; k < 3; k++) {
+        const double o = r.origin.e[k], d = r.dir.e[k];
+        if (!isfinite(o) || !isfinite(d)) return 1;
+        const double lo = c->mb_lo.e[k], hi = c->mb_hi.e[k];
+        if (d == 0.0) {
+            if (o < lo || o > hi) return 0;
+            continue;
+        }
+        double a = (lo - o) / d, b = (hi - o) / d;
+        if (a > b) { const double x = a; a = b; b = x; }
+        a -= fabs(a) * 0x1p-30;
+        b += fabs(b) * 0x1p-30;
+        if (a > t0) t0 = a;
+        if (b < t1) t1 = b;
+    }
+    return t0 <= t1;
+}
+
 /* closest_hit, main.c:52-92 (linear scan: spheres, then triangles) */
 static oracle_hit closest_hit(ctx* c, rt_ray r, int count_tex)
 {
@@ -328,7 +364,12 @@ static oracle_hit closest_hit(ctx* c, rt_ray r, int count_tex)
     }
     int tri_won = 0;
     long long n_texels = (long long)sc->nbMaterials * sc->tex_width * sc->tex_height;
-    for (int i = 0; i < sc->nbTriangles; i++) {
+    int nt = sc->nbTriangles;
+    if (nt > 0 && c->mesh_cull && !meets_mesh_box(c, r)) {   /* no triangle can be hit: the scan finds none */
+        c->cnt[RT_CNT_TRI_TESTS] += (unsigned long long)nt;  /* (the reference's count: it tests them all) */
+        nt = 0;
+    }
+    for (int i = 0; i < nt; i++) {
         const rt_triangle* tri = &sc->triangle_list[i];
         oracle_hit h = hit_triangle(c, tri, r);
         if (h.didHit && h.dst < best.dst) {
@@ -701,6 +742,28 @@ static void init_ctx(ctx* c, const band* b)
     c->sky = b->p->sky_mode == RT_SKY_LAST_SPHERE && b->sc->sky_mat_list && b->sc->nbSpheres > 0;
     c->seed = b->p->seed;
     c->cuda = b->p->semantics == RT_SEM_CUDA;
+    if (!c->cuda && b->sc->nbTriangles > 0 && g_mesh_cull) {
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY}, m = 0.0;
+        int finite = 1;
+        for (int i = 0; i < b->sc->nbTriangles; i++) {
+            const rt_triangle* t = &b->sc->triangle_list[i];
+            const rt_point3* P[3] = {&t->A, &t->B, &t->C};
+            for (int q = 0; q < 3; q++)
+                for (int k = 0; k < 3; k++) {
+                    const double x = P[q]->e[k];
+                    finite = finite && isfinite(x);
+                    lo[k] = fmin(lo[k], x);
+                    hi[k] = fmax(hi[k], x);
+                    m = fmax(m, fabs(x));
+                }
+        }
+        const double pad = 0x1p-16 * (1.0 + m);
+        c->mesh_cull = finite;
+        for (int k = 0; k < 3; k++) {
+            c->mb_lo.e[k] = lo[k] - pad;
+            c->mb_hi.e[k] = hi[k] + pad;
+        }
+    }
     if (c->cuda && b->sc->nbTriangles > 0) {           /* load_geometry_data's box, triangle.hu:142-156 */
         const rt_triangle* t0 = &b->sc->triangle_list[0];
         c->bb_lo = t0->A;

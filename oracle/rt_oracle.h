@@ -40,6 +40,9 @@ int oracle_render_rows(const rt_scene* scene, const rt_params* params,
 /* Force the math library: -1 auto (libm for GLIBC, portable for PHILOX),
  * 0 libm, 1 portable.  Global; for experiments only. */
 void oracle_set_math(int mode);
+/* Speed only: skip the triangle scan of rays that cannot meet the mesh's
+ * padded box (main.c mode; default on, identical frames either way). */
+void oracle_set_mesh_cull(int on);
 
 /* Leaf functions (for parity against the compiled reference headers). */
 oracle_hit oracle_hit_sphere(rt_point3 center, double radius, rt_ray r);

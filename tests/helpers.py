@@ -63,6 +63,18 @@ def sky_tree_scene():
     return SceneBundle(sk.spheres, scenes.moved(scenes.load_tree_fixture(), scenes.TREE_MOVE), sky=sk.sky)
 
 
+def mineways_scene():
+    """mineways_tri.obj (606 triangles, 11 textures incl. alpha leaves) scaled
+    into the README box (as test_gpu_parity.test_mineways_alpha_holes)."""
+    tris, qm, mats, tw, th, nm = scenes.load_mesh_fixture("mineways")
+    for t in tris:
+        for P in (t.A, t.B, t.C):
+            P.e[0] = P.e[0] * 0.1 - 0.2
+            P.e[1] = P.e[1] * 0.1 - 1.0
+            P.e[2] = P.e[2] * 0.1 - 2.5
+    return SceneBundle(scenes.cornell_spheres(), (tris, qm, mats, tw, th, nm))
+
+
 def tree_scene(move=scenes.TREE_MOVE):
     """C4: README spheres + 1tree_tri.obj (1320 tris, Kd-flat materials)."""
     return SceneBundle(scenes.cornell_spheres(), scenes.moved(scenes.load_tree_fixture(), move))
@@ -93,13 +105,18 @@ def oracle_render(bundle, p, row_hi=None, row_lo=0, nthreads=1, counters=False):
     return out
 
 
-def ppm_md5(canva):
+def ppm_text(canva):
+    """The P3 file main.c:457-465 writes (rows top to bottom: j = H-1 .. 0)."""
     H, W, _ = canva.shape
     lines = ["P3\n%d %d\n255\n" % (W, H)]
     for j in range(H - 1, -1, -1):
         row = canva[j].astype(np.int64)
         lines.extend("%d %d %d\n" % (r, g, b) for r, g, b in row)
-    return hashlib.md5("".join(lines).encode()).hexdigest()
+    return "".join(lines)
+
+
+def ppm_md5(canva):
+    return hashlib.md5(ppm_text(canva).encode()).hexdigest()
 
 
 def rmse_per_channel(a, b):

@@ -43,6 +43,7 @@ def oracle():
                                            P(C.c_ulonglong)]
         lib.oracle_render_rows.restype = C.c_int
         lib.oracle_set_math.argtypes = [C.c_int]
+        lib.oracle_set_mesh_cull.argtypes = [C.c_int]
         lib.oracle_hit_sphere.argtypes = [Vec3, C.c_double, Ray]
         lib.oracle_hit_sphere.restype = OracleHit
         lib.oracle_hit_sphere_cuda.argtypes = [Vec3, C.c_double, Ray]

@@ -83,6 +83,7 @@ def test_fp32_close_to_fp64(name):
     c32, a32, n32, r32 = _gpu_render(bundle, p)
     for b in (c32, a32, n32, r32):
         assert (b != -1.0).any(), "fp32 kernel wrote nothing"
+    assert (np.isfinite(r32) == np.isfinite(r64)).all(), "fp32 produced NaN/inf where fp64 did not (or vice versa)"
     r64, r32 = np.nan_to_num(r64), np.nan_to_num(r32)
     m64 = r64.reshape(-1, 3).mean(0)
     m32 = r32.reshape(-1, 3).mean(0)
@@ -94,6 +95,34 @@ def test_fp32_close_to_fp64(name):
     assert (np.abs(m32 - m64) <= REL_MEAN * scale).all()
     assert (mae <= REL_MAE * scale).all()
     assert far <= CANVA_FRAC
+
+
+# north_star's gate: "within 1e-4 per-channel RMSE" of main.c's image on
+# identical seeds.  Here: per-channel RMSE over the full C2 / C3 frame of the
+# pre-gamma radiance (sum / S) and of canva / 255, FP32 kernel against the
+# ORACLE's fp64 image.  Measured r03 (16 / 8 spp): see DESIGN.md §4d -- the
+# FP32 mode does NOT meet 1e-4 (a path whose float decision differs from fp64
+# diverges completely, so the error is Monte-Carlo noise of the diverged
+# samples, ~sigma * sqrt(f / S)).  The assertion bounds it at RMSE_FP32_MAX,
+# so a regression shows; the fp64 default is bit-exact (RMSE 0).
+RMSE_FP32_MAX = 0.05
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["C2", "C3"])
+def test_fp32_rmse_vs_oracle(name):
+    import os
+    bundle, p = {"C2": lambda: (helpers.cornell(), helpers.params(1200, 900, 16, 6, chunks=4)),
+                 "C3": lambda: (helpers.pyramid_scene(), helpers.params(1200, 900, 8, 6, chunks=4))}[name]()
+    ref = helpers.oracle_render(bundle, p, nthreads=max(1, min(16, os.cpu_count() or 1)))
+    p.precision = T.RT_PREC_FP32
+    c32, _, _, r32 = _gpu_render(bundle, p)
+    assert (np.isfinite(r32) == np.isfinite(ref["radiance"])).all()
+    rad = helpers.rmse_per_channel(r32, ref["radiance"])
+    can = helpers.rmse_per_channel(c32 / 255.0, ref["canva"] / 255.0)
+    print("fp32 %s vs oracle fp64: radiance RMSE %s, canva/255 RMSE %s (north_star gate 1e-4)" %
+          (name, np.array2string(rad, precision=6), np.array2string(can, precision=6)))
+    assert (rad <= RMSE_FP32_MAX).all() and (can <= RMSE_FP32_MAX).all()
 
 
 def test_fill_precision_setter_round_trip():

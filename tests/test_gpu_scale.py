@@ -93,6 +93,16 @@ def test_bvh_queue_kernel_c4_band():
         assert_same(got[k], ref[name][400:464], name)
 
 
+def test_bvh_queue_kernel_c4_full_frame():
+    """C4 at its own size: the full 1200x900 frame of the tree scene (1320
+    triangles, AO 2.5 -> 2, 8 bounces) through the BVH task-queue kernel with
+    resumable walks, 2 spp in 2 chunks (2.2 M tasks), every plane bit-exact
+    against the oracle (which scans all 1320 triangles per cast)."""
+    ref = check_parity(helpers.tree_scene(), helpers.params(1200, 900, 2, 8, use_ao=True, chunks=2),
+                       nthreads=ORACLE_THREADS)
+    assert ref["canva"].max() > 0
+
+
 # ---- many tasks per lane: the queue kernel on a few blocks -------------------
 @pytest.mark.parametrize("blocks,case", [(1, "cornell"), (3, "cornell"), (2, "cornell_ao"), (1, "pyramid"),
                                          (5, "aperture"), (2, "tree_ao"), (1, "sweep")])

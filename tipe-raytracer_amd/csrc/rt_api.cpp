@@ -152,6 +152,7 @@ struct rt_device_scene {
     double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0;
     float bvh_rbox = 0.0f;           // >= every |bound| of the BVH's boxes
     bool mats_bounded = false;       // every diffuse/emission/strength finite, |x| <= 2^100
+    bool mats_bounded_f32 = false;   // ... |x| <= 2^50: RT_PREC_FP32's em = emis * es * 1.5 * AO stays < FLT_MAX
     double coord_max = HUGE_VAL;     // max |coordinate| of the spheres (|C_a| + R) and triangle vertices
 };
 
@@ -160,11 +161,11 @@ namespace {
 std::atomic<int> g_zero_exit{1};
 
 // The shading fields a zero rayColor multiplies (LanePath::zero_rc).
-bool shading_bounded(const DevMat& m)
+bool shading_bounded(const DevMat& m, double lim = 0x1p100)
 {
     const double v[7] = {m.dr, m.dg, m.db, m.er, m.eg, m.eb, m.es};
     for (double x : v)
-        if (!(std::fabs(x) <= 0x1p100)) return false;
+        if (!(std::fabs(x) <= lim)) return false;
     return true;
 }
 
@@ -334,7 +335,11 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     cam += 0.5 * (std::fabs(ox) + std::fabs(oy));
     // Zero-throughput exit (rt_kernels.hip LanePath::zero_rc): exact when the
     // shading values are bounded and, with AO, the AO factor stays finite.
+    // RT_PREC_FP32 forms em = emis * es * 1.5 * AO in binary32: with every
+    // shading value within 2^50 (and AO <= 1000) it stays below FLT_MAX, so a
+    // zero rayColor still makes every later bounce add exactly 0.
     kp.zero_exit = g_zero_exit.load() && p->semantics != RT_SEM_CUDA && sc->mats_bounded &&
+                   (p->precision != RT_PREC_FP32 || sc->mats_bounded_f32) &&
                    (!kp.useAO || (AO > 0.0 && AO <= 1000.0 && std::fmax(sc->coord_max, cam) <= 0x1p20));
     if (sc->bvh && p->accel == RT_ACCEL_AUTO && cam <= sc->r_scene) {
         kp.bvh = sc->bvh;
@@ -547,8 +552,12 @@ struct CachedScene {
     std::shared_ptr<rt_device_scene> ds;
     unsigned long long used;
 };
+// The cache is a heap object that is never destroyed: a process that exits
+// without rt_shutdown (main.c's drop-in flow never calls it) must not run
+// free_scene -> hipFree from a static destructor after the HIP runtime may
+// already be torn down; the driver reclaims the device memory at exit.
 std::mutex g_cache_mu;
-std::vector<CachedScene> g_cache;          // at most kCacheEntries, least recently used evicted
+std::vector<CachedScene>& g_cache = *new std::vector<CachedScene>();   // at most kCacheEntries, LRU evicted
 unsigned long long g_cache_clock = 0;
 constexpr size_t kCacheEntries = 4;
 
@@ -633,7 +642,11 @@ void rt_shutdown(void)
 
 const char* rt_last_error(void) { return g_err.c_str(); }
 
-const char* rt_version(void) { return "tipe-raytracer-mi355x 0.2 (abi 1, gfx950, fp64 exact)"; }
+const char* rt_version(void)
+{
+    return "tipe-raytracer-mi355x 0.3 (abi 2, gfx950; precision FP64 bit-exact by default, opt-in RT_PREC_FP32; "
+           "rt_params_init defaults spp_chunks to RT_SPP_CHUNKS_AUTO, a fixed per-pixel slice grouping)";
+}
 
 int rt_device_count(void)
 {
@@ -769,11 +782,13 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         for (long long i = 0; i < n_texels; ++i) texels[(size_t)i] = to_dev(scene->mat_list[i]);
     }
 
-    bool mats_bounded = true;
+    bool mats_bounded = true, mats_bounded_f32 = true;
     double coord_max = 0.0;
-    for (const DevMat& m : sph_mat) mats_bounded = mats_bounded && shading_bounded(m);
-    for (const DevMat& m : texels) mats_bounded = mats_bounded && shading_bounded(m);
-    for (const DevMat& m : sky) mats_bounded = mats_bounded && shading_bounded(m);
+    for (const std::vector<DevMat>* v : {&sph_mat, &texels, &sky})
+        for (const DevMat& m : *v) {
+            mats_bounded = mats_bounded && shading_bounded(m);
+            mats_bounded_f32 = mats_bounded_f32 && shading_bounded(m, 0x1p50);
+        }
     for (int i = 0; i < scene->nbSpheres; ++i) {
         const rt_sphere& q = scene->sphere_list[i];
         for (int a = 0; a < 3; ++a) coord_max = std::fmax(coord_max, std::fabs(q.center.e[a]) + std::fabs(q.radius));
@@ -788,6 +803,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     rt_device_scene* ds = new rt_device_scene();
     ds->device = device;
     ds->mats_bounded = mats_bounded;
+    ds->mats_bounded_f32 = mats_bounded_f32;
     ds->coord_max = coord_max;
     ds->ns = scene->nbSpheres;
     ds->ns_pad = ns_pad;
@@ -903,6 +919,8 @@ int rt_count_async(const rt_device_scene* scene, const rt_params* params, const 
     int rc;
     if ((rc = validate_params(params)) || (rc = validate_tiling(tiling))) return rc;
     if (!d_counters) return fail(RT_EINVAL, "d_counters is NULL");
+    if (params->precision == RT_PREC_FP32)     // the counters instrument the fp64 integrator only
+        return fail(RT_EUNSUPPORTED, "rt_count_async counts the fp64 integrator; precision FP32 has no COUNT build");
     KParams kp;
     double uni[U_COUNT];
     make_kparams(scene, params, tiling, kp, uni);
@@ -929,6 +947,196 @@ int rt_assemble_async(const rt_color* gathered, long long rank_stride, int world
                                   (double*)out, hip_stream);
     if (e) return fail(RT_EDEVICE, "assemble launch: %s", hipGetErrorString((hipError_t)e));
     return RT_OK;
+}
+
+// ---- device-resident multi-device frame ----------------------
+// main_cuda.cu:280-339 renders on one device and copies the three planes to
+// the host.  Several devices of one node: each renders its cyclic row tiles,
+// and the tiles travel device to device over xGMI (peer copies on the
+// destination's copy engines: a gather into one device is G-1 point-to-point
+// transfers, which is all ncclGather, rccl.h:745, would issue for it inside one
+// process), then the assemble kernel un-permutes them into row order.
+namespace {
+
+void enable_peer(int dst, int src)
+{
+    if (dst == src) return;
+    static std::mutex mu;
+    static std::vector<std::pair<int, int>> done;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto& d : done)
+        if (d.first == dst && d.second == src) return;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, dst, src) == hipSuccess && can) {
+        DeviceGuard g(dst);
+        const hipError_t e = hipDeviceEnablePeerAccess(src, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    }
+    done.emplace_back(dst, src);     // without peer access the runtime stages the copy itself
+}
+
+// One plane: slot r's rows_per_rank*W colours (device src_dev[r]) into the
+// rank-major staging block r on dst_dev, then assemble into out (W*H).
+int gather_plane(int world, const int* src_dev, const rt_color* const* locals, int tile_rows, int rows_per_rank,
+                 int W, int H, int dst_dev, rt_color* staging, rt_color* out, hipStream_t st)
+{
+    const size_t n = (size_t)rows_per_rank * W;
+    for (int r = 0; r < world; ++r) {
+        if (!locals[r]) return fail(RT_EINVAL, "locals[%d] is NULL", r);
+        enable_peer(dst_dev, src_dev[r]);
+        const hipError_t e = hipMemcpyPeerAsync(staging + (size_t)r * n, dst_dev, locals[r], src_dev[r],
+                                                n * sizeof(rt_color), st);
+        if (e != hipSuccess) return fail(RT_EDEVICE, "peer copy %d -> %d: %s", src_dev[r], dst_dev, hipGetErrorString(e));
+    }
+    const int e = launch_assemble((const double*)staging, (long long)n, world, tile_rows, rows_per_rank, W, H,
+                                  (double*)out, st);
+    if (e) return fail(RT_EDEVICE, "assemble launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+int check_gather_geometry(int world, int tile_rows, int rows_per_rank, int W, int H)
+{
+    if (world < 1 || tile_rows < 1 || rows_per_rank < 0 || W < 1 || H < 1 || rows_per_rank % tile_rows)
+        return fail(RT_EINVAL, "bad gather geometry");
+    const long long tiles = (H + tile_rows - 1) / tile_rows;
+    if ((long long)world * (rows_per_rank / tile_rows) < tiles)
+        return fail(RT_EINVAL, "%d ranks x %d tiles < %lld tiles", world, rows_per_rank / tile_rows, tiles);
+    return RT_OK;
+}
+
+}  // namespace
+
+int rt_gather_async(int world, const int* src_devices, const rt_color* const* locals, int tile_rows,
+                    int rows_per_rank, int W, int H, int dst_device, rt_color* out, void* hip_stream)
+{
+    int rc;
+    if (!src_devices || !locals || !out) return fail(RT_EINVAL, "NULL argument");
+    if ((rc = check_gather_geometry(world, tile_rows, rows_per_rank, W, H))) return rc;
+    DeviceGuard g(dst_device);
+    hipStream_t st = (hipStream_t)hip_stream;
+    rt_color* staging = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&staging, (size_t)world * rows_per_rank * W * sizeof(rt_color), st));
+    rc = gather_plane(world, src_devices, locals, tile_rows, rows_per_rank, W, H, dst_device, staging, out, st);
+    (void)hipFreeAsync(staging, st);
+    return rc;
+}
+
+int rt_render_gather_async(const rt_scene* scene, const rt_params* params, int tile_rows, const rt_frame* frame,
+                           void* hip_stream)
+{
+    int rc;
+    if ((rc = validate_scene(scene)) || (rc = validate_params(params))) return rc;
+    if (!frame || !frame->canva) return fail(RT_EINVAL, "frame.canva is NULL");
+    if (tile_rows < 1) return fail(RT_EINVAL, "tile_rows %d < 1", tile_rows);
+    std::vector<int> devs;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if ((rc = ensure_init_locked())) return rc;
+        devs = g_devices;
+    }
+    const int G = (int)devs.size(), W = params->largeur_image, H = params->hauteur_image;
+    const int dst = devs[0];
+    const int n_tiles = (((H + tile_rows - 1) / tile_rows) + G - 1) / G;      // per slot (rows >= H skipped)
+    const int rows_pr = n_tiles * tile_rows;
+    rt_color* outs[4] = {frame->canva, frame->albedo, frame->normal, frame->radiance};
+    int nplanes = 0;
+    for (rt_color* o : outs) nplanes += o ? 1 : 0;
+    const size_t plane = (size_t)rows_pr * W;                            // colours per plane and slot
+    hipStream_t dst_st = (hipStream_t)hip_stream;
+
+    struct Slot {
+        std::shared_ptr<rt_device_scene> sc;
+        PooledStream* ps = nullptr;
+        rt_color* buf = nullptr;
+        hipEvent_t ev = nullptr;
+    };
+    std::vector<Slot> slots((size_t)G);
+    auto release = [&]() {           // stream-ordered: nothing here waits for the GPU
+        for (auto& s : slots) {
+            if (!s.ps) continue;
+            DeviceGuard g(s.ps->device);
+            if (s.buf) (void)hipFreeAsync(s.buf, s.ps->st);
+            if (s.ev) (void)hipEventDestroy(s.ev);
+            stream_pool_put(s.ps);
+            s.ps = nullptr;
+        }
+    };
+    // 1. every slot renders its tiles on its own device and pooled stream,
+    //    after whatever the caller enqueued on hip_stream before this call
+    hipEvent_t go = nullptr;
+    {
+        DeviceGuard g(dst);
+        HIP_TRY(hipEventCreateWithFlags(&go, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(go, dst_st));
+    }
+    for (int q = 0; q < G && rc == RT_OK; ++q) {
+        Slot& s = slots[(size_t)q];
+        if ((rc = scene_cache_get(devs[(size_t)q], scene, s.sc)) || (rc = stream_pool_get(devs[(size_t)q], &s.ps))) break;
+        DeviceGuard g(devs[(size_t)q]);
+        hipError_t e = hipStreamWaitEvent(s.ps->st, go, 0);
+        if (e == hipSuccess) e = hipMallocAsync((void**)&s.buf, plane * nplanes * sizeof(rt_color), s.ps->st);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&s.ev, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            rc = fail(RT_EDEVICE, "device %d frame: %s", devs[(size_t)q], hipGetErrorString(e));
+            break;
+        }
+        rt_tiling t{0, tile_rows, q, G, n_tiles};
+        KParams kp;
+        double uni[U_COUNT];
+        make_kparams(s.sc.get(), params, &t, kp, uni);
+        rt_color* nxt = s.buf;
+        double** dstp[4] = {&kp.canva, &kp.albedo, &kp.normal, &kp.radiance};
+        for (int pl = 0; pl < 4; ++pl) {
+            *dstp[pl] = outs[pl] ? (double*)nxt : nullptr;
+            if (outs[pl]) nxt += plane;
+        }
+        if ((rc = launch_on_stream(kp, uni, s.ps->st, false))) break;
+        if ((e = hipEventRecord(s.ev, s.ps->st)) != hipSuccess)
+            rc = fail(RT_EDEVICE, "device %d event: %s", devs[(size_t)q], hipGetErrorString(e));
+    }
+    // 2. the destination's stream waits for every slot, gathers each plane over
+    //    xGMI and un-permutes it; 3. each slot frees its planes after the copies
+    if (rc == RT_OK) {
+        DeviceGuard g(dst);
+        for (int q = 0; q < G && rc == RT_OK; ++q) {
+            const hipError_t e = hipStreamWaitEvent(dst_st, slots[(size_t)q].ev, 0);
+            if (e != hipSuccess) rc = fail(RT_EDEVICE, "wait: %s", hipGetErrorString(e));
+        }
+        rt_color* staging = nullptr;
+        if (rc == RT_OK) {
+            const hipError_t e = hipMallocAsync((void**)&staging, (size_t)G * plane * sizeof(rt_color), dst_st);
+            if (e != hipSuccess) rc = fail(RT_ENOMEM, "gather staging: %s", hipGetErrorString(e));
+        }
+        int k = 0;
+        for (int pl = 0; pl < 4 && rc == RT_OK; ++pl) {
+            if (!outs[pl]) continue;
+            std::vector<const rt_color*> loc((size_t)G);
+            for (int q = 0; q < G; ++q) loc[(size_t)q] = slots[(size_t)q].buf + (size_t)k * plane;
+            rc = gather_plane(G, devs.data(), loc.data(), tile_rows, rows_pr, W, H, dst, staging, outs[pl], dst_st);
+            ++k;
+        }
+        if (staging) (void)hipFreeAsync(staging, dst_st);
+        if (rc == RT_OK) {
+            const hipError_t e = hipEventRecord(go, dst_st);     // reused: "the copies are done"
+            for (int q = 0; q < G && e == hipSuccess; ++q) {
+                DeviceGuard gq(devs[(size_t)q]);
+                (void)hipStreamWaitEvent(slots[(size_t)q].ps->st, go, 0);
+            }
+        }
+    }
+    if (rc != RT_OK) {               // keep the error message; make every slot idle before freeing
+        for (auto& s : slots)
+            if (s.ps) {
+                DeviceGuard gq(s.ps->device);
+                (void)hipStreamSynchronize(s.ps->st);
+            }
+    }
+    release();
+    {
+        DeviceGuard g(dst);
+        (void)hipEventDestroy(go);
+    }
+    return rc;
 }
 
 int rt_render_rows(const rt_scene* scene, const rt_params* params, int row_hi, int row_lo, rt_color* canva,

@@ -102,9 +102,13 @@ struct Philox {
 // (three-input xor; k a wave-uniform SGPR)
 __device__ __forceinline__ uint32_t xor3_s(uint32_t a, uint32_t b, uint32_t k)
 {
+#if defined(__gfx950__)
     uint32_t r;
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
     return r;
+#else
+    return a ^ b ^ k;                  // other targets: the compiler's own xor chain
+#endif
 }
 
 template <bool UNIFORM_KEY = true>

@@ -6,8 +6,10 @@
 // sample chunking, one 72-byte partial sum per pixel and chunk).
 //
 // Semantics follow main.c (the authoritative CPU path), not main_cuda.cu:
-//   fill_canva        main.c:245-284      -> render_kernel / combine_kernel
-//   tracer            main.c:118-242      -> trace()
+//   fill_canva        main.c:245-284      -> render_kernel_q (task queue) /
+//                                            render_kernel (fixed grid), combine_kernel
+//   tracer            main.c:118-242      -> QPath (queue kernel), LanePath
+//                                            (fixed grid), samples_f32 (FP32 mode)
 //   closest_hit       main.c:52-92        -> closest_hit()
 //   ambient_occlusion main.c:94-116       -> ao_factor()
 //   hit_sphere        sphere.h:13-47      -> sphere_exact() (+ candidate pass)
@@ -30,7 +32,7 @@
 //    result never depends on the approximation;
 //  * per-lane divergent data (the winner's material, texels) is fetched once
 //    per bounce from L1/L2;
-//  * the IOR stack of pile.h reduces to one register (top n2), see trace();
+//  * the IOR stack of pile.h reduces to one register (top n2), see QPath::finish_bounce;
 //  * albedo/normal are final once the primary chain (camera ray through
 //    alpha holes) ends, so they are added to the accumulators there instead
 //    of being carried through the bounce loop;
@@ -65,15 +67,10 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
-#ifndef RT_BVH_COOP                 // BVH kernel: wave-cooperative deep traversal once this many
-#define RT_BVH_COOP 1               // lanes wait for it (0: off, each lane walks its own tree)
-#endif
-#ifndef RT_FLAT                     // sphere kernel: sample loop as LanePath rounds (0: nested trace())
-#define RT_FLAT 1
-#endif
-#ifndef RT_FLAT_FILL                // ... camera rays start once this many eighths of the live lanes wait
-#define RT_FLAT_FILL 2
-#endif
+#define RT_BVH_COOP 1               // fixed-grid BVH kernel: wave-cooperative deep traversal once this
+                                    // many lanes wait for it (samples_coop)
+#define RT_FLAT_FILL 2              // fixed-grid sphere kernel: camera rays start once this many eighths
+                                    // of the live lanes wait (samples_flat)
 #ifndef RT_QUEUE                    // sphere kernel, spp_chunks > 1: persistent lanes + (chunk, pixel) task queue
 #define RT_QUEUE 64                 // (tasks per atomic grab of a wave; 0: off)
 #endif
@@ -145,21 +142,6 @@ __device__ __forceinline__ KParamsK kp_here()
     return p;
 }
 
-// Cost-attribution knobs (tools/attribute_costs.sh): RT_DUP_<part> runs a
-// part twice on opaque copies of its inputs and keeps the first result, so
-// the measured slowdown is that part's cost.  Off in every shipped build.
-__device__ __forceinline__ bool opaque_false()
-{
-    int z = 0;
-    asm volatile("" : "+v"(z));
-    return z != 0;
-}
-template <class T>
-__device__ __forceinline__ T launder(T x)
-{
-    asm volatile("" : "+v"(x));
-    return x;
-}
 
 // (int) of a double as the reference's x86-64 build executes it (cvttsd2si):
 // NaN and out-of-range values give INT_MIN, the "integer indefinite".  C
@@ -185,16 +167,6 @@ __device__ __forceinline__ Mat load_mat(const DevMat* m)
 // per thread ([9][256], conflict-free), so they occupy no VGPRs across the
 // bounce loop.  Only the owning thread touches its column: plain
 // read-add-write, same IEEE adds in the same order as fill_canva's sums.
-__device__ __forceinline__ V3 lds_get(const double* acc, int base)
-{
-    return v3(acc[(base + 0) * 256], acc[(base + 1) * 256], acc[(base + 2) * 256]);
-}
-__device__ __forceinline__ void lds_put(double* acc, int base, V3 v)
-{
-    acc[(base + 0) * 256] = v.x;
-    acc[(base + 1) * 256] = v.y;
-    acc[(base + 2) * 256] = v.z;
-}
 __device__ __forceinline__ void acc_add(double* acc, int base, V3 v)
 {
     acc[(base + 0) * 256] = acc[(base + 0) * 256] + v.x;
@@ -202,40 +174,7 @@ __device__ __forceinline__ void acc_add(double* acc, int base, V3 v)
     acc[(base + 2) * 256] = acc[(base + 2) * 256] + v.z;
 }
 
-enum : int { ACC_RAD = 0, ACC_ALB = 3, ACC_NRM = 6, ACC_INC = 9, ACC_RC = 12, ACC_SLOTS = 15 };
-
-// incomingLight / rayColor of tracer (main.c:124-125).  In LDS slots 9..14
-// for the sphere kernel (touched once per bounce, frees 12 VGPRs across the
-// hit scans); in registers for the BVH kernel, whose LDS budget goes to the
-// traversal stack (4 blocks/CU need <= 40 KB each).
-template <bool IN_LDS>
-struct PathState;
-template <>
-struct PathState<true> {
-    double* acc;
-    __device__ void init()
-    {
-        // constants materialised here (laundered): hoisted out of the sample
-        // loop they were held in VGPRs and spilled to scratch by every wave
-        const double z = launder(0.0), one = launder(1.0);
-        lds_put(acc, ACC_INC, v3(z, z, z));
-        lds_put(acc, ACC_RC, v3(one, one, one));
-    }
-    __device__ V3 inc() const { return lds_get(acc, ACC_INC); }
-    __device__ V3 rc() const { return lds_get(acc, ACC_RC); }
-    __device__ void set_inc(V3 v) { lds_put(acc, ACC_INC, v); }
-    __device__ void set_rc(V3 v) { lds_put(acc, ACC_RC, v); }
-};
-template <>
-struct PathState<false> {
-    double* acc;
-    V3 i_, r_;
-    __device__ void init() { i_ = v3(0, 0, 0); r_ = v3(1, 1, 1); }
-    __device__ V3 inc() const { return i_; }
-    __device__ V3 rc() const { return r_; }
-    __device__ void set_inc(V3 v) { i_ = v; }
-    __device__ void set_rc(V3 v) { r_ = v; }
-};
+enum : int { ACC_RAD = 0, ACC_ALB = 3, ACC_NRM = 6, ACC_SLOTS = 9 };
 
 // Per-thread event counters (COUNT instantiation only).
 struct Cnt {
@@ -414,14 +353,6 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
         const SphGeo s = kp.sph[bk];
         if (sphere_exact<CU>(s.cx, s.cy, s.cz, s.r2, o, d, two_a, four_a, fast, rc2a, t)) win = bk;
         else amb = true;     // cannot happen within the bound; stay exact anyway
-#ifdef RT_DUP_WINNER
-        {
-            double t2;
-            const bool w2 = sphere_exact<CU>(s.cx, s.cy, s.cz, s.r2, v3(launder(o.x), launder(o.y), launder(o.z)),
-                                             d, two_a, four_a, fast, rc2a, t2);
-            if (opaque_false()) { t = t2; amb = !w2; }
-        }
-#endif
     }
     if (amb) {               // exact reference scan for this ray
         if (COUNT) cnt.c[RT_CNT_EXACT_RESCANS] += 1;
@@ -587,17 +518,6 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
     bool h[4];
     float tn[4];
     box4(kp, nd, r32, cull32(kp, best), h, tn);
-#ifdef RT_DUP_BOX
-    {
-        bool h2[4];
-        float tn2[4];
-        Ray32 q = r32;
-        q.ax = launder(q.ax);
-        box4(kp, nd, q, cull32(kp, best), h2, tn2);
-        if (opaque_false())
-            for (int c = 0; c < 4; ++c) { h[c] = h2[c]; tn[c] = tn2[c]; }
-    }
-#endif
     int next = -1;
     float tnext = 0.0f;
     unsigned lm = 0;                                     // hit leaf slots
@@ -635,14 +555,6 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
             if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)(kend - k);
         }
         tri_test<COUNT, CU>(kp, k, o, d, best, kind, win, win_orig);
-#ifdef RT_DUP_TRILEAF
-        {
-            double b2 = best;
-            int k2 = kind, w2 = win, o2 = win_orig;
-            tri_test<COUNT, CU>(kp, k, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2);
-            if (opaque_false()) { best = b2; kind = k2; win = w2; win_orig = o2; }
-        }
-#endif
         ++k;
     }
     if (next >= 0) {
@@ -697,16 +609,6 @@ __device__ __forceinline__ int cast_spheres(const KParams& kp, const V3 o, const
         wave_slots(cnt, RT_CNT_CAST_LANE_SLOTS);
     }
     int win = spheres_closest<COUNT, CU, AMGM>(kp, o, d, a, two_a, four_a, fast, rc2a, best, cnt);
-#ifdef RT_DUP_SPHERES
-    {
-        double b2;
-        const int w2 = spheres_closest<COUNT, CU, AMGM>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, a, two_a,
-                                                  four_a, fast, rc2a, b2, cnt);
-        const bool f = opaque_false();
-        best = f ? b2 : best;
-        win = f ? w2 : win;
-    }
-#endif
     return win;
 }
 
@@ -722,28 +624,8 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
         // main_cuda.cu:40-45: the ray misses the mesh box, no triangle tested
     } else if (BVH) {
         tris_bvh<COUNT, CU>(kp, o, d, best, kind, win, win_orig, cnt);
-#ifdef RT_DUP_TRIS
-        {
-            double b2 = best;
-            int k2 = kind, w2 = win, o2 = win_orig;
-            tris_bvh<COUNT, CU>(kp, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2, cnt);
-            const bool f = opaque_false();
-            best = f ? b2 : best;
-            kind = f ? k2 : kind;
-            win = f ? w2 : win;
-        }
-#endif
     } else {
         for (int k = 0; k < kp.nt; ++k) tri_test<COUNT, CU>(kp, k, o, d, best, kind, win, win_orig);
-#ifdef RT_DUP_SCAN
-        {
-            double b2 = best;
-            int k2 = kind, w2 = win, o2 = win_orig;
-            for (int k = 0; k < kp.nt; ++k)
-                tri_test<COUNT, CU>(kp, k, v3(launder(o.x), launder(o.y), launder(o.z)), d, b2, k2, w2, o2);
-            if (opaque_false()) { best = b2; kind = k2; win = w2; win_orig = o2; }
-        }
-#endif
     }
     t_best = best;
     idx = win;
@@ -828,22 +710,7 @@ __device__ __forceinline__ V3 sampler_vec(double u, double v)
         const double phi = pm_acos(xv);
         pm_sincosf((float)phi, sp_, cp_);
     }
-#ifdef RT_DUP_ACOS
-    {
-        float a, c2;
-        const bool ok = phi_sincosf_fast(launder(xv), a, c2);
-        if (opaque_false()) { sp_ = a; cp_ = ok ? c2 : a; }
-    }
-#endif
     pm_sincosf((float)theta, st_, ct_);
-#ifdef RT_DUP_SINCOS
-    {
-        float a, b;
-        pm_sincosf(launder((float)theta), a, b);
-        const bool f = opaque_false();
-        st_ = f ? a : st_; ct_ = f ? b : ct_;
-    }
-#endif
     return v3((double)(ct_ * sp_), (double)(st_ * sp_), (double)cp_);
 }
 
@@ -855,12 +722,6 @@ __device__ __forceinline__ V3 random_dir(Stream& st, Cnt& cnt)
     const double u = unit31(st.next31());
     const double v = unit31(st.next31());
     const V3 dir = sampler_vec(u, v);
-#ifdef RT_DUP_NORMALIZE
-    {
-        const V3 a = normalize_unit(dir), b = normalize_unit(v3(launder(dir.x), launder(dir.y), launder(dir.z)));
-        return opaque_false() ? b : a;
-    }
-#endif
     return normalize_unit(dir);
 }
 
@@ -937,122 +798,6 @@ __device__ __forceinline__ double ao_factor(const KParams& kp, const V3 p, const
         occ = occ + att;
     }
     return (occ / 1.0) / AO;
-}
-
-// tracer, main.c:118-242, adding its (radiance, albedo, normal) to the
-// accumulators.
-//
-// IOR stack (pile.h): every translucent hit pushes (top.n2, m)
-// (index_suivant_pile) and, when leaving, pops that same pair again, so the
-// stack only changes on entry and only its top n2 is ever read: one register.
-//
-// Albedo/normal (main.c:137-150,159): they are assigned only while
-// i == alpha_depth, i.e. along the primary chain of consecutive alpha holes,
-// and the next chain bounce always overwrites them; they are final when the
-// chain ends (first non-hole bounce, a miss, a light, or the last bounce).
-template <bool COUNT, bool BVH, bool SKY>
-__device__ __forceinline__ void trace(const KParams& kp, V3 o, V3 d, Stream& st, double* acc, Cnt& cnt)
-{
-    PathState<!BVH> ps{acc};
-    ps.init();
-    bool chain = true;
-    double top_n2 = 1.0;
-    if (kp.B <= 0) {                                     // tracer returns (0, 0, 0) albedo/normal
-        acc_add(acc, 3, v3(0, 0, 0));
-        acc_add(acc, 6, v3(0, 0, 0));
-    }
-    for (int i = 0; i < kp.B; i++) {
-        double t;
-        int idx;
-        const int kind = closest_hit<COUNT, BVH>(kp, o, d, t, idx, cnt);
-        if (COUNT) wave_slots(cnt, RT_CNT_SHADE_LANE_SLOTS);
-        if (kind == HIT_NONE) {                          // miss: the path ends, main.c:236-238
-            if (chain) {                                 // albedo/normal of a missed chain ray: 0
-                acc_add(acc, 3, v3(0, 0, 0));            // (main.c:137-140 reads uninitialised
-                acc_add(acc, 6, v3(0, 0, 0));            //  fields; defined as 0)
-            }
-            break;
-        }
-        V3 hp, hn;
-        Mat mat;
-        if (kind == HIT_SPHERE) {
-            const SphGeo s = kp.sph[idx];
-            hp = o + muls(d, t);                         // ray_at
-            hn = normalize(hp - v3(s.cx, s.cy, s.cz));
-            mat = load_mat(kp.sph_mat + idx);
-            if (SKY && idx == kp.ns - 1) sky_material(kp, idx, s, hp, mat);
-        } else {
-            if (COUNT) cnt.c[RT_CNT_TEX_HITS] += 1;
-            const TriGeo g = kp.tri[idx];
-            hp = o + muls(d, t);
-            hn = normalize(v3(g.nx, g.ny, g.nz));
-            mat = tri_material(kp, idx, hp, hn);
-        }
-        if (chain) {
-            // albedo/normal of this chain bounce are final unless it is an
-            // alpha hole with bounces left (then the next bounce overwrites)
-            if (mat.es > 0) {                            // direct view of a light, main.c:154-160
-                const V3 col = hsl_roundtrip(mat.emis);
-                acc_add(acc, 0, col);
-                acc_add(acc, 3, col);
-                acc_add(acc, 6, hn);
-                return;
-            }
-            if (!(mat.alpha < 0.0001) || i == kp.B - 1) {
-                acc_add(acc, 3, mat.diff);
-                acc_add(acc, 6, hn);
-                chain = mat.alpha < 0.0001;              // stays on only for a last-bounce hole
-            }
-        }
-        o = hp;
-        const V3 diffuse_dir = normalize(hn + random_dir<COUNT>(st, cnt));
-        const V3 reflected_dir = d - muls(hn, 2 * dot(d, hn));
-        const V3 dr = diffuse_dir + muls(reflected_dir - diffuse_dir, mat.rs);
-        if (mat.alpha < 0.0001) continue;                // alpha hole: pass through, main.c:200-206
-        chain = false;
-        if (mat.alpha <= 0.99) {                         // refraction, main.c:167-193 (alpha >= 1e-4 here)
-            if (COUNT) cnt.c[RT_CNT_REFRACT] += 1;
-            V3 nn = hn;
-            double n1, n2;
-            if (dot(d, hn) > 0) {                        // leaving: pop restores the stack
-                nn = v3(-hn.x, -hn.y, -hn.z);
-                n1 = mat.ior;
-                n2 = top_n2;
-            } else {                                     // entering: push (top.n2, ior)
-                n1 = top_n2;
-                n2 = mat.ior;
-                top_n2 = mat.ior;
-            }
-            const V3 refr = refracted(d, nn, n1, n2);
-            const double rnd = 0.0 + 1.0 * unit31(st.next31());
-            if (rnd > mat.alpha) {
-                d = refr;
-                continue;
-            }
-            d = dr;
-        } else if (mat.alpha > 0.99) {
-            d = dr;
-        }
-        V3 rc = ps.rc();
-        if (kp.useAO) {
-            // AO_intensity read here (laundered index): hoisted, pm_pow's
-            // exponent analysis ran and spilled once per sample without AO
-            const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
-            const V3 em = muls(mat.emis, mat.es * 1.5 * AO);
-            ps.set_inc(ps.inc() + mulv(em, rc));
-            if (rc.x > 0.5 || rc.y > 0.5 || rc.z > 0.5) rc = mulv(mat.diff, muls(rc, 1.3));
-            rc = mulv(mat.diff, rc);
-            ps.set_rc(rc);
-            const double occ = ao_factor<COUNT, BVH>(kp, hp, hn, AO, st, cnt);
-            ps.set_rc(mulv(ps.rc(), v3(occ, occ, occ)));
-        } else {
-            const V3 em = muls(mat.emis, mat.es);
-            ps.set_inc(ps.inc() + mulv(em, rc));
-            if (rc.x > 0.5 || rc.y > 0.5 || rc.z > 0.5) rc = mulv(mat.diff, muls(rc, 1.3));
-            ps.set_rc(mulv(mat.diff, rc));
-        }
-    }
-    acc_add(acc, ACC_RAD, ps.inc());
 }
 
 // tracer, main_cuda.cu:86-141 (rt.h RT_SEM_CUDA).  A pre-pass cast returns
@@ -1195,13 +940,13 @@ __device__ __forceinline__ void camera_ray(const KParams& kp, int x, int g, ST& 
 }
 
 // Resumable trace for the BVH kernel: the same tracer and
-// ambient_occlusion arithmetic as trace() + ao_factor(), as a per-lane state
+// ambient_occlusion arithmetic (main.c:94-242), as a per-lane state
 // machine (LanePath).  A lane in
 //   SM_RESOLVE shades the hit of its finished cast (a bounce or an AO cast),
 //   SM_CAM     starts its next sample (or is done),
 //   SM_CAST    runs the sphere half of the next cast and sets up traversal,
 //   SM_TRAV    visits nodes of the triangle BVH,
-// and a lane's casts, draws and sums happen in the same order as in trace(),
+// and a lane's casts, draws and sums happen in the same order as in tracer,
 // so results are bit-identical.  samples_coop runs it (the fixed-grid BVH
 // kernel: spp_chunks 1, trees too deep for the queue kernel's stacks); r01's
 // samples_sm (each lane at most 4 node visits per round) is superseded by the
@@ -1488,14 +1233,13 @@ struct LanePath {
 
 
 
-#if RT_FLAT > 0
-// The sphere kernel's sample loop as LanePath rounds (RT_FLAT > 0): each
+// The fixed-grid sphere kernel's sample loop as LanePath rounds: each
 // round every lane with a path casts and shades one bounce; a lane whose path
 // ended (a miss, a light seen directly, the bounce budget, or zero
 // throughput) waits for its next sample's camera ray, which starts once
 // RT_FLAT_FILL eighths of the wave's live lanes wait (the camera ray then
 // costs the wave one pass for many lanes).  Same casts, draws and sums per
-// sample as trace(), so bit-identical; it lets the zero-throughput exit
+// sample as tracer, so bit-identical; it lets the zero-throughput exit
 // save the cast instead of idling the lane until the wave's longest path.
 template <bool COUNT, bool SKY>
 __device__ __forceinline__ void samples_flat(const KParams& kp, int x, int g, uint32_t pixel, int s0, int s1,
@@ -1513,10 +1257,8 @@ __device__ __forceinline__ void samples_flat(const KParams& kp, int x, int g, ui
         }
     }
 }
-#endif
 
-#if RT_BVH_COOP > 0
-// Wave-cooperative traversal of the deep casts (RT_BVH_COOP > 0).  About 5 %
+// Wave-cooperative traversal of the deep casts (fixed-grid BVH kernel).  About 5 %
 // of C4's casts go below the tree's root; walked by their own lanes they
 // keep a wave at a few active lanes for ~25 node visits and ~12 triangle
 // tests (leaf loop 2.6 % lane efficiency).  Here a lane runs its cast's root
@@ -1529,7 +1271,7 @@ __device__ __forceinline__ void samples_flat(const KParams& kp, int x, int g, ui
 // into the owner's record in a wave-uniform loop with the same rule as
 // tri_test (strictly closer, or an equal-dst triangle with a smaller caller
 // index; a sphere keeps an equal-dst hit).  That rule is a total order, so
-// the winner is the one trace() finds, whatever order the triangles are
+// the winner is the one tracer finds, whatever order the triangles are
 // tested in; culling against an older `best` only tests more boxes.
 __device__ __forceinline__ double rl_d(double v, int l)
 {
@@ -1778,7 +1520,6 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
         for (int j = 0; j < 11; ++j) atomicAdd(kp.trace + j, qs[j]);
 #endif
 }
-#endif
 
 // n / d and n % d for 32-bit n by a launch-constant d with m = kp's
 // floor((2^32 - 1) / d) (host, qdiv_magic): the high product is q or q - 1,
@@ -1832,7 +1573,7 @@ __device__ __forceinline__ void render_body(const KParams& kp)
         const uint32_t pixel = (uint32_t)g * (uint32_t)kp.W + (uint32_t)x;
         const int s0 = chunk_start(kp.S, kp.chunks, kp.chunk_taper, kp.chunk_den, 0u, (unsigned)chunk);
         const int s1 = chunk_start(kp.S, kp.chunks, kp.chunk_taper, kp.chunk_den, 0u, (unsigned)chunk + 1u);
-        __shared__ double acc_lds[(BVH ? ACC_INC : ACC_SLOTS) * 256];
+        __shared__ double acc_lds[ACC_SLOTS * 256];
         __shared__ uint32_t rng_lds[4 * 256];
         double* acc = acc_lds + threadIdx.x;
         const long long li = (long long)ly * kp.W + x;
@@ -1841,26 +1582,21 @@ __device__ __forceinline__ void render_body(const KParams& kp)
         const bool carry = !COUNT && kp.sums && kp.chunks == 1;
 #pragma unroll
         for (int j = 0; j < 9; ++j) acc[j * 256] = carry ? kp.sums[li * 9 + j] : 0.0;
-#if RT_BVH_COOP > 0
         if constexpr (BVH && !CU) {
             samples_coop<COUNT, SKY>(kp, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc, cnt);
-        } else
-#endif
-#if RT_FLAT > 0
-        if constexpr (!BVH && !CU) {
+        } else if constexpr (!BVH && !CU) {
             samples_flat<COUNT, SKY>(kp, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc, cnt);
-        } else
-#endif
-        for (int s = s0; s < s1; ++s) {
-            Stream st;
-            st.start(pixel, (uint32_t)(kp.s_base + s), kp.key0, kp.key1, rng_lds + threadIdx.x);
-            V3 no, rd;
-            camera_ray<CU>(kp, x, g, st, no, rd);
-            if (CU) trace_cuda<COUNT, BVH>(kp, no, rd, st, acc, cnt);
-            else trace<COUNT, BVH, SKY>(kp, no, rd, st, acc, cnt);
-            if (COUNT) {
-                cnt.c[RT_CNT_SAMPLES] += 1;
-                cnt.c[RT_CNT_RNG_DRAWS] += st.n;
+        } else {                             // CU: main_cuda.cu's nested sample loop (main_cuda.cu:150-165)
+            for (int s = s0; s < s1; ++s) {
+                Stream st;
+                st.start(pixel, (uint32_t)(kp.s_base + s), kp.key0, kp.key1, rng_lds + threadIdx.x);
+                V3 no, rd;
+                camera_ray<CU>(kp, x, g, st, no, rd);
+                trace_cuda<COUNT, BVH>(kp, no, rd, st, acc, cnt);
+                if (COUNT) {
+                    cnt.c[RT_CNT_SAMPLES] += 1;
+                    cnt.c[RT_CNT_RNG_DRAWS] += st.n;
+                }
             }
         }
         if (!COUNT) {
@@ -2361,7 +2097,7 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
 //                 the direction draws), AO set-up
 // The draws keep the reference's per-sample order (counter-based stream:
 // direction n, n+1, refraction n+2, AO next), so results are bit-identical
-// to trace(); work whose result cannot reach the output is skipped: the
+// to tracer; work whose result cannot reach the output is skipped: the
 // direction after the last bounce, and the AO cast of the last bounce
 // (tracer multiplies rayColor by it and then returns incomingLight).
 enum : int { ROLE_NONE = 0, ROLE_BOUNCE = 1, ROLE_CAMERA = 2 };
@@ -2577,7 +2313,7 @@ struct QPath {
 template <bool SKY, int AOM, int QB>
 __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
 {
-    __shared__ double acc_lds[ACC_INC * 256];
+    __shared__ double acc_lds[ACC_SLOTS * 256];
     __shared__ uint32_t rng_lds[4 * 256];
     double* acc = acc_lds + threadIdx.x;
     uint32_t* rng = rng_lds + threadIdx.x;

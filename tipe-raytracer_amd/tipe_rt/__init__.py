@@ -58,6 +58,9 @@ def lib():
         L.rt_count_async.argtypes = [C.c_void_p, P(Params), P(Tiling), C.c_void_p, C.c_void_p]
         L.rt_assemble_async.argtypes = [C.c_void_p, C.c_longlong, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_void_p, C.c_void_p]
+        L.rt_gather_async.argtypes = [C.c_int, P(C.c_int), P(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_int, C.c_void_p, C.c_void_p]
+        L.rt_render_gather_async.argtypes = [P(Scene), P(Params), C.c_int, P(Frame), C.c_void_p]
         L.rt_selftest_math.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         L.rt_verify_sampler_phi.argtypes = [C.c_ulonglong, C.c_ulonglong, C.c_void_p]
         L.rt_verify_sphere_pass.argtypes = [P(Scene), C.c_void_p, C.c_longlong, C.c_void_p]
@@ -87,7 +90,7 @@ EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error",
                     "rt_selftest_math", "rt_accumulate_async", "rt_resolve_async", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
                     "rt_denoise_unpack", "rt_denoise_pack_async", "rt_verify_sampler_phi",
                     "rt_verify_sphere_pass", "rt_verify_normalize", "rt_set_zero_throughput_exit", "rt_set_fill_spp_chunks", "rt_set_fill_precision",
-                    "rt_scene_cache_clear"]
+                    "rt_scene_cache_clear", "rt_gather_async", "rt_render_gather_async"]
 
 # rt_denoise_fn (rt.h): denoiser()'s signature, denoiser.h:31
 DENOISE_FN = C.CFUNCTYPE(None, C.c_int, C.c_int, C.c_void_p, Camera, C.c_void_p, C.c_void_p)
@@ -281,6 +284,23 @@ def count_async(dscene, params, tiling, counters_ptr, stream=None):
 def assemble_async(gathered_ptr, world, tile_rows, rows_per_rank, W, H, out_ptr, stream=None, rank_stride=0):
     check(lib().rt_assemble_async(gathered_ptr, rank_stride, world, tile_rows, rows_per_rank, W, H, out_ptr,
                                   stream))
+
+
+def gather_async(src_devices, local_ptrs, tile_rows, rows_per_rank, W, H, dst_device, out_ptr, stream=None):
+    """rt_gather_async: slot r's local plane (device src_devices[r]) -> out on
+    dst_device over peer copies, un-permuted into row order."""
+    n = len(src_devices)
+    devs = (C.c_int * n)(*src_devices)
+    locs = (C.c_void_p * n)(*local_ptrs)
+    check(lib().rt_gather_async(n, devs, locs, tile_rows, rows_per_rank, W, H, dst_device, out_ptr, stream))
+
+
+def render_gather_async(scene, params, tile_rows, canva_ptr, albedo_ptr=None, normal_ptr=None, radiance_ptr=None,
+                        stream=None):
+    """rt_render_gather_async: every device of rt_init's list renders its
+    cyclic tiles; the planes are gathered into the first device's frame."""
+    fr = Frame(canva_ptr, albedo_ptr, normal_ptr, radiance_ptr)
+    check(lib().rt_render_gather_async(C.byref(scene), C.byref(params), tile_rows, C.byref(fr), stream))
 
 
 def verify_sampler_phi(r0=0, n=1 << 31):
