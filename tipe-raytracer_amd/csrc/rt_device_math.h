@@ -150,13 +150,7 @@ struct Stream {
         const uint32_t slot = n & 3u;
         uint32_t w;
         if (slot == 0u) {
-            Philox blk = philox4x32_10(n >> 2, 0u, pixel, sample, k0, k1);
-#ifdef RT_DUP_PHILOX
-            uint32_t m = 0, px2 = pixel;
-            asm volatile("" : "+v"(m), "+v"(px2));
-            const Philox b2 = philox4x32_10(n >> 2, 0u, px2, sample, k0, k1);
-            blk.w0 ^= (b2.w0 ^ b2.w1 ^ b2.w2 ^ b2.w3) & m;
-#endif
+            const Philox blk = philox4x32_10(n >> 2, 0u, pixel, sample, k0, k1);
             cache[256] = blk.w1;
             cache[512] = blk.w2;
             cache[768] = blk.w3;

@@ -78,10 +78,7 @@ static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) m
 #ifndef RT_WAVES_PER_SIMD_Q         // queue kernel occupancy bound
 #define RT_WAVES_PER_SIMD_Q RT_WAVES_PER_SIMD
 #endif
-#ifndef RT_QSTATS                   // diagnostic build: round census of render_kernel_q in the trace
-#define RT_QSTATS 0
-#endif
-#define RT_TRACE_WORDS (RT_QSTATS ? 18 : 4)
+#define RT_TRACE_WORDS 4                // RT_QUEUE_TRACE words per lane: start, end, rounds, tasks
 #ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
 #define RT_WAVES_PER_SIMD_BVH 3
 #endif
@@ -967,9 +964,6 @@ struct LanePath {
     double top_n2, best;
     int i, kind, win, win_orig, node, sp, s, state;
     bool chain, ao_cast;
-#if RT_QSTATS
-    bool dbg_lit = false, dbg_phi_fb = false;    // diagnostic build: this round's lit branch / phi fallback
-#endif
 
     // Zero-throughput exit (kp.zero_exit, set by the host only when it is
     // exact): once rayColor is (0, 0, 0) every later bounce adds em * 0 = +-0
@@ -1056,9 +1050,6 @@ struct LanePath {
                     acc_add(acc, ACC_ALB, col);
                     acc_add(acc, ACC_NRM, hn);
                     lit = true;
-#if RT_QSTATS
-                    dbg_lit = true;
-#endif
                 } else if (!(mat.alpha < 0.0001) || i == kp.B - 1) {
                     acc_add(acc, ACC_ALB, mat.diff);
                     acc_add(acc, ACC_NRM, hn);
@@ -1388,48 +1379,16 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
     const int lane = threadIdx.x & 63;
     LanePath<COUNT, SKY> L;
     L.init(s0, s1);
-#if RT_QSTATS
-    // diagnostic build: [0] loop rounds [1] coop phases [2] coop iterations
-    // [3] lanes with a task per coop iteration [4] parked lanes per phase
-    // [5] lanes resolving [6] lanes starting [7] lanes casting; time [8]
-    // resolve+start [9] cast+root [10] coop
-    unsigned long long qs[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tq = __builtin_amdgcn_s_memtime();
-#define QTB(slot)                                                  \
-    {                                                              \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-        qs[slot] += t_ - tq;                                       \
-        tq = t_;                                                   \
-    }
-#else
-#define QTB(slot)
-#endif
     while (L.state != SM_DONE) {
-#if RT_QSTATS
-        qs[0] += 1;
-        qs[5] += (unsigned long long)__popcll(__ballot(L.state == SM_RESOLVE));
-#endif
         if (L.state == SM_RESOLVE) L.resolve(kp, acc, cnt);
-#if RT_QSTATS
-        qs[6] += (unsigned long long)__popcll(__ballot(L.state == SM_CAM));
-#endif
         if (L.state == SM_CAM) L.start(kp, x, g, pixel, s1, rng, acc, cnt);
-        QTB(8)
-#if RT_QSTATS
-        qs[7] += (unsigned long long)__popcll(__ballot(L.state == SM_CAST));
-#endif
         if (L.state == SM_CAST) {
             L.cast(kp, cnt);
             L.trav(kp, stk, 1, cnt);             // the root node; SM_TRAV: parked
         }
-        QTB(9)
         const unsigned long long parked = __ballot(L.state == SM_TRAV);
         const unsigned long long movable = __ballot(L.state == SM_RESOLVE || L.state == SM_CAM);
         if (parked == 0ull || (__popcll(parked) < RT_BVH_COOP && movable != 0ull)) continue;
-#if RT_QSTATS
-        qs[1] += 1;
-        qs[4] += (unsigned long long)__popcll(parked);
-#endif
 
         // ---- cooperative phase (wave-uniform) ----
         int qn = 0;
@@ -1448,9 +1407,6 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
         V3 to = v3(0, 0, 0), td = to;
         Ray32 tr32 = Ray32{0, 0, 0, 0, 0, 0, 0, 0, 0};
         for (;;) {
-#if RT_QSTATS
-            qs[2] += 1;
-#endif
             const unsigned long long idle = __ballot(!has);
             const int take = min(__popcll(idle), qn);
             bool fresh = false;
@@ -1468,9 +1424,6 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
             qn -= take;
             __builtin_amdgcn_wave_barrier();
             if (__ballot(has) == 0ull) break;
-#if RT_QSTATS
-            qs[3] += (unsigned long long)__popcll(__ballot(has));
-#endif
             // the owner's ray for new tasks, its current record for every task
             // (all live lanes run the permutes; owners are live)
             if (__ballot(fresh) != 0ull) {
@@ -1513,12 +1466,7 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
             }
         }
         if (L.state == SM_TRAV) L.state = SM_RESOLVE;
-        QTB(10)
     }
-#if RT_QSTATS
-    if (kp.trace && (threadIdx.x & 63) == 0)
-        for (int j = 0; j < 11; ++j) atomicAdd(kp.trace + j, qs[j]);
-#endif
 }
 
 // n / d and n % d for 32-bit n by a launch-constant d with m = kp's
@@ -2310,6 +2258,200 @@ struct QPath {
     }
 };
 
+// One lane of the queue kernels outside its path: the task it runs (chunk,
+// pixel of the band), the wave's batch of tasks and the draw stream of the
+// sample in flight.  take_tasks and next_ray are steps 3 and 4 of a round of
+// render_kernel_q and render_kernel_qc.
+template <bool SKY, int AOM>
+struct QLane {
+    QPath<SKY, AOM> L;
+    Stream st;                       // draws of the sample in flight (next31 for refraction / AO)
+    int x, g, s1;
+    unsigned chunk, p, pixel;
+    unsigned qb, qe;                 // the wave's batch of tasks [qb, qe) (wave-uniform)
+    unsigned ntasks;
+    bool owns;                       // the lane's LDS sums belong to task (chunk, p)
+
+    __device__ __forceinline__ void init(const KParams& kp, uint32_t* rng)
+    {
+        L.o = L.d = L.cd = L.inc = L.rc = v3(0, 0, 0);
+        L.top_n2 = 1.0;
+        L.best = 0.0;
+        L.i = 0; L.kind = HIT_NONE; L.win = -1; L.s = 0;
+        L.chain = true; L.ao_cast = false;
+        L.state = SM_CAM;            // s = 0 >= s1 = 0: takes a task first
+        x = g = s1 = 0;
+        chunk = p = pixel = 0;
+        qb = qe = 0;
+        ntasks = 0;
+        owns = false;
+        st.start(0u, 0u, kp.key0, kp.key1, rng);
+    }
+
+    // ---- 3. lanes whose task is done take the next one ----------------------
+    // Tasks come from a per-launch counter, RT_QUEUE per atomic: the wave
+    // takes a batch and hands its tasks to its lanes as they need them.
+    __device__ __forceinline__ void take_tasks(double* acc, int lane)
+    {
+        const bool need = L.state == SM_CAM && L.s >= s1;
+        const unsigned long long nm = __ballot(need);
+        if (!nm) return;             // wave-uniform
+        // launch constants re-read here (SMEM) instead of living in SGPRs
+        // spilled to VGPR lanes across the whole round
+        const KParamsK K = kp_here();
+        unsigned t = 0;
+        const unsigned nn = (unsigned)__popcll(nm), avail = qe - qb;
+        const unsigned rank = (unsigned)__popcll(nm & ((1ull << lane) - 1ull));
+        if (avail < nn) {            // a new batch (nn <= 64 <= RT_QUEUE): old tasks first
+            unsigned nb = 0;
+            if (lane == __ffsll((long long)nm) - 1) nb = atomicAdd(K->task_ctr, (unsigned)RT_QUEUE);
+            nb = __shfl(nb, __ffsll((long long)nm) - 1, 64);
+            t = rank < avail ? qb + rank : nb + (rank - avail);
+            qb = nb + (nn - avail);
+            qe = nb + RT_QUEUE;
+        } else {
+            t = qb + rank;
+            qb += nn;
+        }
+        if (!need) return;
+        ++ntasks;
+        if (owns) {                  // task done: its sums to the chunk partials
+            double* q = K->partial + ((size_t)chunk * ((unsigned)K->band_rows * (unsigned)K->W) + p) * 9;
+#pragma unroll
+            for (int j = 0; j < 9; ++j) q[j] = acc[j * 256];
+            owns = false;
+        }
+        if (t >= K->npx_here * (unsigned)K->chunks) {
+            L.state = SM_DONE;
+            return;
+        }
+        // task t = (chunk, pixel p of the band): launch-constant divisors
+        chunk = udiv_q(t, K->npx_here, K->qm_npx, p);
+        unsigned xr;
+        const unsigned row = udiv_q(p, (unsigned)K->W, K->qm_w, xr);
+        const int ly = K->band_y0 + (int)row;
+        x = (int)xr;
+        bool valid = ly < K->local_rows;
+        if (valid) {
+            unsigned yy;
+            const int lt = (int)udiv_q((unsigned)ly, (unsigned)K->tile_rows, K->qm_tile, yy);
+            g = K->row_base + (K->tile_first + lt * K->tile_step) * K->tile_rows + (int)yy;
+            valid = g < K->row_end;
+        }
+        if (valid) {                 // otherwise the lane takes its next task next round
+            pixel = (uint32_t)g * (uint32_t)K->W + (uint32_t)x;
+            L.s = chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk);
+            s1 = chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk + 1u);
+#pragma unroll
+            for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
+            owns = true;
+        }
+    }
+
+    // tracer with nbRebondMax <= 0 returns (0, 0, 0) albedo/normal/colour:
+    // one sample of the task; false when the lane has no such sample
+    __device__ __forceinline__ bool empty_sample(const KParams& kp, double* acc)
+    {
+        if (!(kp.B <= 0 && L.state == SM_CAM && L.s < s1)) return false;
+        acc_add(acc, ACC_ALB, v3(0, 0, 0));
+        acc_add(acc, ACC_NRM, v3(0, 0, 0));
+        acc_add(acc, ACC_RAD, v3(0, 0, 0));
+        ++L.s;
+        return true;
+    }
+
+    // ---- 4. next ray: bounce direction or camera ray (shared work) --------
+    __device__ __forceinline__ void next_ray(const KParams& kp, int role, const QHit& H, double* acc, uint32_t* rng)
+    {
+        if (role == ROLE_NONE) return;
+        const bool cam = role == ROLE_CAMERA;
+        // draws: a bounce uses draws n, n+1 of its sample (rtutility.h:
+        // 189-203); a camera ray draws 0-3 of sample s (main.c:265-269)
+        const uint32_t nd = cam ? 0u : st.n;
+        const uint32_t sa = nd & 3u, sb = (nd + 1u) & 3u;
+        uint32_t wa = 0, wb = 0;
+        if (!cam && sa != 0u) wa = rng[sa * 256];          // cached word of the current block
+        if (!cam && sb != 0u && sa != 0u) wb = rng[sb * 256];
+        Philox blk{0, 0, 0, 0};
+        if (cam || sa == 0u || sb == 0u) {                 // a new block: one Philox for both roles
+            const uint32_t bi = cam ? 0u : ((nd + (sa == 0u ? 0u : 1u)) >> 2);
+            blk = philox4x32_10(bi, 0u, pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1);
+            if (!cam) {                                     // keep the rest of the block
+                rng[256] = blk.w1;
+                rng[512] = blk.w2;
+                rng[768] = blk.w3;
+            }
+        }
+        if (!cam) {
+            if (sa == 0u) wa = blk.w0;
+            if (sb == 0u) wb = blk.w0;
+            else if (sa == 0u) wb = blk.w1;
+        }
+        V3 X;
+        V3 no = v3(0, 0, 0);
+        if (cam) {
+            CamDraws w{blk, 0};
+            const double ju = -0.5 + 1.0 * unit31(w.next31());     // randomDouble(-0.5, 0.5)
+            const double jv = -0.5 + 1.0 * unit31(w.next31());
+            const int b = opq0();
+            const cdptr U = (cdptr)kp.uni;
+            const double nu = (double)x + ju, nv = (double)g + jv;
+            const double rcw = U[b + U_RC_WM1], rch = U[b + U_RC_HM1];
+            const double u = rcw != 0.0 ? div_core(nu, U[b + U_WM1], rcw) : nu / U[b + U_WM1];
+            const double v = rch != 0.0 ? div_core(nv, U[b + U_HM1], rch) : nv / U[b + U_HM1];
+            const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
+            const V3 ch = v3(U[b + U_CAM_H], U[b + U_CAM_H + 1], U[b + U_CAM_H + 2]);
+            const V3 cv = v3(U[b + U_CAM_V], U[b + U_CAM_V + 1], U[b + U_CAM_V + 2]);
+            const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
+            const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));     // get_ray, camera.h:42-55
+            const V3 dest = co + muls(dir, U[b + U_FOCUS]);
+            if (kp.cam_pin) {                              // zero aperture: the origin itself (host-checked)
+                no = co;
+            } else {
+                const double jx = -0.5 + 1.0 * unit31(w.next31());
+                const double jy = -0.5 + 1.0 * unit31(w.next31());
+                const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
+                no = co + v3(dx, dy, 0);
+            }
+            X = dest - no;
+        } else {
+            // random_dir_no_norm (rtutility.h:189-203), then n + dir (main.c:163)
+            const double u = unit31(wa >> 1);
+            const double v = unit31(wb >> 1);
+            X = H.hn + normalize_unit(sampler_vec(u, v));
+            st.n += 2;
+        }
+        const V3 dn = normalize(X);
+        if (cam) {                                         // the new sample's primary ray
+            L.o = no;
+            L.d = dn;
+            if (AOM == AO_ON) L.cd = dn;
+            L.inc = v3(0, 0, 0);
+            L.rc = v3(1, 1, 1);
+            L.top_n2 = 1.0;
+            L.i = 0;
+            L.chain = true;
+            L.ao_cast = false;
+            L.state = SM_CAST;
+            st.start(pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1, rng);
+            st.n = 4;                                      // draws 0-3 were the camera's
+        } else {
+            L.finish_bounce(kp, dn, st, acc, H);
+        }
+    }
+
+    // per lane start, end, rounds, tasks (RT_QUEUE_TRACE diagnostics)
+    __device__ __forceinline__ void trace_out(const KParams& kp, long long t_start, unsigned rounds) const
+    {
+        if (!kp.trace) return;
+        unsigned long long* q = kp.trace + ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
+        q[0] = (unsigned long long)t_start;
+        q[1] = (unsigned long long)wall_clock64();
+        q[2] = rounds;
+        q[3] = ntasks;
+    }
+};
+
 template <bool SKY, int AOM, int QB>
 __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
 {
@@ -2318,20 +2460,10 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     double* acc = acc_lds + threadIdx.x;
     uint32_t* rng = rng_lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
-    unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
-    QPath<SKY, AOM> L;
-    L.o = L.d = L.cd = L.inc = L.rc = v3(0, 0, 0);
-    L.top_n2 = 1.0;
-    L.best = 0.0;
-    L.i = 0; L.kind = HIT_NONE; L.win = -1; L.s = 0;
-    L.chain = true; L.ao_cast = false;
-    L.state = SM_CAM;                // s = 0 >= s1 = 0: takes a task first
-    int x = 0, g = 0, s1 = 0;
+    QLane<SKY, AOM> Q;
+    Q.init(kp, rng);
+    QPath<SKY, AOM>& L = Q.L;
     int node = 0, sp = 0, win_orig = 0;      // BVH walk in flight (state SM_TRAV)
-    unsigned chunk = 0, p = 0, pixel = 0;
-    bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
-    Stream st;                       // draw stream of the sample in flight (next31 for refraction / AO)
-    st.start(0u, 0u, kp.key0, kp.key1, rng);
     // shallow trees (QB 4: depth4 <= 4, e.g. the 50-node sweep tree) keep
     // their top nodes in LDS: sweep +5.7 %; deep ones gain nothing (C4 -0.5 %)
     constexpr int NTOP = QB == 4 ? RT_QB_TOP : 0;
@@ -2343,28 +2475,9 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
         __syncthreads();
     }
     const long long t_start = kp.trace ? wall_clock64() : 0;
-    unsigned rounds = 0, ntasks = 0;
-#if RT_QSTATS
-    // diagnostic build only: [0] rounds [1] lanes casting [2] lanes BOUNCE
-    // [3] lanes CAMERA [4] task rounds [5] lanes taking a task; time [8] cast
-    // [9] resolve_hit [10] tasks [11] next_ray [12] finish
-    unsigned long long qs[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tq = __builtin_amdgcn_s_memtime();
-#define QT(slot)                                                   \
-    {                                                              \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-        qs[slot] += t_ - tq;                                       \
-        tq = t_;                                                   \
-    }
-#else
-#define QT(slot)
-#endif
+    unsigned rounds = 0;
     while (true) {
         ++rounds;
-#if RT_QSTATS
-        qs[0] += 1;
-        qs[1] += (unsigned long long)__popcll(__ballot(L.state == SM_CAST));
-#endif
         // ---- 1. closest hit (main.c:52-92) for every lane with a ray ------
         if (QB > 0) {
             // spheres, then the triangle BVH: up to QB node visits
@@ -2380,7 +2493,6 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 sp = 0;
                 L.state = SM_TRAV;
             }
-            QT(13)
             if (__ballot(L.state == SM_TRAV) != 0ull) {
                 const V3 dd = L.cast_dir();
                 const Ray32 r32 = ray32(L.o, dd, kp.bvh_rbox);
@@ -2388,10 +2500,6 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 const BvhNode4* top = NTOP > 0 ? bvh_top_q() : nullptr;
 #pragma unroll 1
                 for (int j = 0; j < QB; ++j) {
-#if RT_QSTATS
-                    qs[6] += 1;
-                    qs[7] += (unsigned long long)__popcll(__ballot(L.state == SM_TRAV));
-#endif
                     if (L.state == SM_TRAV) {
                         Cnt cnt;
                         if (!bvh_step<false, false, NTOP>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind, L.win,
@@ -2406,7 +2514,6 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
             L.kind = closest_hit<false, false, false, !SKY && AOM != AO_ON>(kp, L.o, L.cast_dir(), L.best, L.win, cnt);
             L.state = SM_RESOLVE;
         }
-        QT(8)
         // ---- 2. the hit, up to the next direction --------------------------
         int role = ROLE_NONE;
         QHit H;
@@ -2414,172 +2521,181 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
         H.rs = 0.0;
         H.refr = H.hole = false;
         if (L.state == SM_RESOLVE) role = L.resolve_hit(kp, acc, H);
-        QT(9)
         // ---- 3. lanes whose task is done take the next one -----------------
-        const bool need = L.state == SM_CAM && L.s >= s1;
-        const unsigned long long nm = __ballot(need);
-        if (nm) {                    // wave-uniform: tasks for the lanes that need one
-            // launch constants re-read here (SMEM) instead of living in SGPRs
-            // spilled to VGPR lanes across the whole round
-            const KParamsK K = kp_here();
-#if RT_QSTATS
-            qs[4] += 1;
-            qs[5] += (unsigned long long)__popcll(nm);
-#endif
-            unsigned t = 0;
-            const unsigned nn = (unsigned)__popcll(nm), avail = qe - qb;
-            const unsigned rank = (unsigned)__popcll(nm & ((1ull << lane) - 1ull));
-            if (avail < nn) {        // a new batch (nn <= 64 <= RT_QUEUE): old tasks first
-                unsigned nb = 0;
-                if (lane == __ffsll((long long)nm) - 1) nb = atomicAdd(K->task_ctr, (unsigned)RT_QUEUE);
-                nb = __shfl(nb, __ffsll((long long)nm) - 1, 64);
-                t = rank < avail ? qb + rank : nb + (rank - avail);
-                qb = nb + (nn - avail);
-                qe = nb + RT_QUEUE;
-            } else {
-                t = qb + rank;
-                qb += nn;
-            }
-            if (need) {
-                ++ntasks;
-                if (owns) {          // task done: its sums to the chunk partials
-                    double* q = K->partial + ((size_t)chunk * ((unsigned)K->band_rows * (unsigned)K->W) + p) * 9;
-#pragma unroll
-                    for (int j = 0; j < 9; ++j) q[j] = acc[j * 256];
-                    owns = false;
-                }
-                if (t >= K->npx_here * (unsigned)K->chunks) {
-                    L.state = SM_DONE;
-                } else {
-                    // task t = (chunk, pixel p of the band): launch-constant divisors
-                    chunk = udiv_q(t, K->npx_here, K->qm_npx, p);
-                    unsigned xr;
-                    const unsigned row = udiv_q(p, (unsigned)K->W, K->qm_w, xr);
-                    const int ly = K->band_y0 + (int)row;
-                    x = (int)xr;
-                    bool valid = ly < K->local_rows;
-                    if (valid) {
-                        unsigned yy;
-                        const int lt = (int)udiv_q((unsigned)ly, (unsigned)K->tile_rows, K->qm_tile, yy);
-                        g = K->row_base + (K->tile_first + lt * K->tile_step) * K->tile_rows + (int)yy;
-                        valid = g < K->row_end;
-                    }
-                    if (valid) {     // otherwise the lane takes its next task next round
-                        pixel = (uint32_t)g * (uint32_t)K->W + (uint32_t)x;
-                        L.s = chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk);
-                        s1 = chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk + 1u);
-#pragma unroll
-                        for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
-                        owns = true;
-                    }
-                }
-            }
-        }
+        Q.take_tasks(acc, lane);
         if (__ballot(L.state != SM_DONE) == 0ull) break;     // every lane of the wave is done
-        // tracer with nbRebondMax <= 0 returns (0, 0, 0) albedo/normal/colour
-        if (kp.B <= 0 && L.state == SM_CAM && L.s < s1) {
-            acc_add(acc, ACC_ALB, v3(0, 0, 0));
-            acc_add(acc, ACC_NRM, v3(0, 0, 0));
-            acc_add(acc, ACC_RAD, v3(0, 0, 0));
-            ++L.s;
-            continue;
-        }
-        if (L.state == SM_CAM && L.s < s1) role = ROLE_CAMERA;
-        QT(10)
-#if RT_QSTATS
-        qs[2] += (unsigned long long)__popcll(__ballot(role == ROLE_BOUNCE));
-        qs[3] += (unsigned long long)__popcll(__ballot(role == ROLE_CAMERA));
-#endif
+        if (Q.empty_sample(kp, acc)) continue;
+        if (L.state == SM_CAM && L.s < Q.s1) role = ROLE_CAMERA;
         // ---- 4. next ray: bounce direction or camera ray (shared work) ----
-        if (role != ROLE_NONE) {
-            const bool cam = role == ROLE_CAMERA;
-            // draws: a bounce uses draws n, n+1 of its sample (rtutility.h:
-            // 189-203); a camera ray draws 0-3 of sample s (main.c:265-269)
-            const uint32_t nd = cam ? 0u : st.n;
-            const uint32_t sa = nd & 3u, sb = (nd + 1u) & 3u;
-            uint32_t wa = 0, wb = 0;
-            if (!cam && sa != 0u) wa = rng[sa * 256];          // cached word of the current block
-            if (!cam && sb != 0u && sa != 0u) wb = rng[sb * 256];
-            Philox blk{0, 0, 0, 0};
-            if (cam || sa == 0u || sb == 0u) {                 // a new block: one Philox for both roles
-                const uint32_t bi = cam ? 0u : ((nd + (sa == 0u ? 0u : 1u)) >> 2);
-                blk = philox4x32_10(bi, 0u, pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1);
-                if (!cam) {                                     // keep the rest of the block
-                    rng[256] = blk.w1;
-                    rng[512] = blk.w2;
-                    rng[768] = blk.w3;
-                }
-            }
-            if (!cam) {
-                if (sa == 0u) wa = blk.w0;
-                if (sb == 0u) wb = blk.w0;
-                else if (sa == 0u) wb = blk.w1;
-            }
-            V3 X;
-            V3 no = v3(0, 0, 0);
-            if (cam) {
-                CamDraws w{blk, 0};
-                const double ju = -0.5 + 1.0 * unit31(w.next31());     // randomDouble(-0.5, 0.5)
-                const double jv = -0.5 + 1.0 * unit31(w.next31());
-                const int b = opq0();
-                const cdptr U = (cdptr)kp.uni;
-                const double nu = (double)x + ju, nv = (double)g + jv;
-                const double rcw = U[b + U_RC_WM1], rch = U[b + U_RC_HM1];
-                const double u = rcw != 0.0 ? div_core(nu, U[b + U_WM1], rcw) : nu / U[b + U_WM1];
-                const double v = rch != 0.0 ? div_core(nv, U[b + U_HM1], rch) : nv / U[b + U_HM1];
-                const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
-                const V3 ch = v3(U[b + U_CAM_H], U[b + U_CAM_H + 1], U[b + U_CAM_H + 2]);
-                const V3 cv = v3(U[b + U_CAM_V], U[b + U_CAM_V + 1], U[b + U_CAM_V + 2]);
-                const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
-                const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));     // get_ray, camera.h:42-55
-                const V3 dest = co + muls(dir, U[b + U_FOCUS]);
-                if (kp.cam_pin) {                              // zero aperture: the origin itself (host-checked)
-                    no = co;
-                } else {
-                    const double jx = -0.5 + 1.0 * unit31(w.next31());
-                    const double jy = -0.5 + 1.0 * unit31(w.next31());
-                    const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
-                    no = co + v3(dx, dy, 0);
-                }
-                X = dest - no;
-            } else {
-                // random_dir_no_norm (rtutility.h:189-203), then n + dir (main.c:163)
-                const double u = unit31(wa >> 1);
-                const double v = unit31(wb >> 1);
-                X = H.hn + normalize_unit(sampler_vec(u, v));
-                st.n += 2;
-            }
-            const V3 dn = normalize(X);
-            QT(11)
-            if (cam) {                                         // the new sample's primary ray
-                L.o = no;
-                L.d = dn;
-                if (AOM == AO_ON) L.cd = dn;
-                L.inc = v3(0, 0, 0);
-                L.rc = v3(1, 1, 1);
-                L.top_n2 = 1.0;
-                L.i = 0;
-                L.chain = true;
-                L.ao_cast = false;
-                L.state = SM_CAST;
-                st.start(pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1, rng);
-                st.n = 4;                                      // draws 0-3 were the camera's
-            } else {
-                L.finish_bounce(kp, dn, st, acc, H);
+        Q.next_ray(kp, role, H, acc, rng);
+    }
+    Q.trace_out(kp, t_start, rounds);
+}
+
+// ---- BVH scenes: closest hits compacted over the block (render_kernel_qc) --
+// In render_kernel_q<.., QB> a lane whose ray walks the tree spends whole
+// rounds in SM_TRAV while its wave runs the other lanes' path work, and the
+// walks themselves run with the wave's other lanes idle (C4: lane
+// utilisation 0.35).  Here the closest hit of every cast (main.c:52-92: the
+// sphere candidate pass, then up to QB node visits of the triangle BVH) is
+// taken out of the owner lane: each round
+//   A. (each wave, its own lanes) a finished cast's hit goes back to its
+//      owner, which shades it, takes tasks and makes its next ray (the same
+//      QPath / QLane steps as render_kernel_q), then posts the ray: o and the
+//      cast direction into the owner's LDS slot, the owner's id into its
+//      wave's list;
+//   B. block barrier;
+//   C. the block's posted casts -- new ones and walks in flight -- are dealt
+//      densely over its 256 threads (item i to thread (i + 64 r) mod 256, the
+//      start wave r rotating by round and block so no SIMD always gets the
+//      remainder); a thread runs its item's sphere pass if the cast is new
+//      and up to QB node visits, and stores the walk state (node, stack
+//      pointer, best, winner) back into the owner's slot; the stack stays the
+//      owner's LDS column;
+//   D. block barrier.
+// Every cast is the same closest_hit arithmetic, only run by another lane of
+// the block, so frames are bit-identical to render_kernel_q's.  Waves whose
+// lanes are all done keep looping as tracers until the whole block is done
+// (the loop exit is block-uniform, so every wave reaches every barrier).
+// LDS 52 KiB per block (sums, Philox cache, stacks, ray slots): 3 blocks per CU.
+#ifndef RT_WAVES_PER_SIMD_QC
+#define RT_WAVES_PER_SIMD_QC 3
+#endif
+template <bool SKY, int AOM, int QB>
+__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_QC) void render_kernel_qc(const KParams kp)
+{
+    __shared__ double acc_lds[ACC_SLOTS * 256];
+    __shared__ uint32_t rng_lds[4 * 256];
+    __shared__ double ray_lds[6 * 256];          // owner t's cast: o.x o.y o.z d.x d.y d.z at [k * 256 + t]
+    __shared__ double best_lds[256];             // its closest t so far
+    __shared__ int wst_lds[3 * 256];             // [t] node | sp << 16 | kind << 24 | QC_NEW | QC_DONE;
+                                                 // [256 + t] winner; [512 + t] winner's caller index
+    __shared__ unsigned short list_lds[256];     // wave w's posted owners at [64 w, 64 w + n_w)
+    __shared__ int wave_lds[8];                  // [w] n_w; [4 + w] wave w has lanes with work
+    constexpr int QC_NEW = 1 << 26, QC_DONE = 1 << 27;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double* acc = acc_lds + tid;
+    uint32_t* rng = rng_lds + tid;
+    unsigned short* stk0 = bvh_stack_q() - tid;  // column c: stk0 + c
+    QLane<SKY, AOM> Q;
+    Q.init(kp, rng);
+    QPath<SKY, AOM>& L = Q.L;
+    unsigned rot = blockIdx.x & 3u;
+    const long long t_start = kp.trace ? wall_clock64() : 0;
+    unsigned rounds = 0;
+    while (true) {
+        ++rounds;
+        // ---- A. owner phase --------------------------------------------------
+        if (L.state == SM_TRAV) {                // a posted cast: done in the last C phase?
+            const int w0 = wst_lds[tid];
+            if (w0 & QC_DONE) {
+                L.best = best_lds[tid];
+                L.kind = (w0 >> 24) & 3;
+                L.win = wst_lds[256 + tid];
+                L.state = SM_RESOLVE;
             }
         }
-        QT(12)
+        int role = ROLE_NONE;
+        QHit H;
+        H.hn = v3(0, 0, 0);
+        H.rs = 0.0;
+        H.refr = H.hole = false;
+        if (L.state == SM_RESOLVE) role = L.resolve_hit(kp, acc, H);
+        Q.take_tasks(acc, lane);
+        if (!Q.empty_sample(kp, acc)) {
+            if (L.state == SM_CAM && L.s < Q.s1) role = ROLE_CAMERA;
+            Q.next_ray(kp, role, H, acc, rng);
+        }
+        if (L.state == SM_CAST) {                // post the cast
+            const V3 dd = L.cast_dir();
+            ray_lds[tid] = L.o.x;
+            ray_lds[256 + tid] = L.o.y;
+            ray_lds[512 + tid] = L.o.z;
+            ray_lds[768 + tid] = dd.x;
+            ray_lds[1024 + tid] = dd.y;
+            ray_lds[1280 + tid] = dd.z;
+            wst_lds[tid] = QC_NEW;
+            L.state = SM_TRAV;
+        }
+        // wave w's new casts at list [64 w, 64 w + n_w), its walks in flight
+        // from 64 w + 63 down: the block's items are all new casts first (their
+        // sphere pass then runs on whole waves), then the walks
+        const bool fresh = L.state == SM_TRAV && wst_lds[tid] == QC_NEW;
+        const bool cont = L.state == SM_TRAV && !fresh;
+        const unsigned long long fm = __ballot(fresh), cm = __ballot(cont);
+        const unsigned long long below = (1ull << lane) - 1ull;
+        if (fresh) list_lds[wave * 64 + __popcll(fm & below)] = (unsigned short)tid;
+        if (cont) list_lds[wave * 64 + 63 - __popcll(cm & below)] = (unsigned short)tid;
+        const unsigned long long live = __ballot(L.state != SM_DONE);
+        if (lane == 0) {
+            wave_lds[wave] = __popcll(fm) | (__popcll(cm) << 8);
+            wave_lds[4 + wave] = live != 0ull;
+        }
+        __syncthreads();
+        // ---- C. tracer phase: the block's casts over its threads -------------
+        if ((wave_lds[4] | wave_lds[5] | wave_lds[6] | wave_lds[7]) == 0) break;   // block-uniform
+        const int v0 = wave_lds[0], v1 = wave_lds[1], v2 = wave_lds[2], v3_ = wave_lds[3];
+        const int f0 = v0 & 255, f1 = v1 & 255, f2 = v2 & 255, f3 = v3_ & 255;
+        const int nf = f0 + f1 + f2 + f3;
+        const int n_items = nf + (v0 >> 8) + (v1 >> 8) + (v2 >> 8) + (v3_ >> 8);
+        const int it = (tid - 64 * (int)rot) & 255;
+        rot = (rot + 1u) & 3u;
+        if (it < n_items) {
+            // item it: the it-th new cast, else the (it - nf)-th walk, in wave order
+            const bool isnew = it < nf;
+            const int c0 = isnew ? f0 : v0 >> 8, c1 = isnew ? f1 : v1 >> 8, c2 = isnew ? f2 : v2 >> 8;
+            int k = isnew ? it : it - nf, w = 0;
+            if (k >= c0) {
+                k -= c0;
+                w = 1;
+                if (k >= c1) {
+                    k -= c1;
+                    w = 2;
+                    if (k >= c2) {
+                        k -= c2;
+                        w = 3;
+                    }
+                }
+            }
+            const int ow = list_lds[isnew ? w * 64 + k : w * 64 + 63 - k];
+            const V3 o = v3(ray_lds[ow], ray_lds[256 + ow], ray_lds[512 + ow]);
+            const V3 dd = v3(ray_lds[768 + ow], ray_lds[1024 + ow], ray_lds[1280 + ow]);
+            const int w0 = wst_lds[ow];
+            double best;
+            int kind, win, win_orig, node, sp;
+            if (w0 & QC_NEW) {                   // spheres first (main.c:59-78)
+                Cnt cnt;
+                win = cast_spheres<false, false>(kp, o, dd, best, cnt);
+                kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
+                win_orig = 0;
+                node = 0;
+                sp = 0;
+            } else {
+                best = best_lds[ow];
+                kind = (w0 >> 24) & 3;
+                win = wst_lds[256 + ow];
+                win_orig = wst_lds[512 + ow];
+                node = w0 & 0xffff;
+                sp = (w0 >> 16) & 0xff;
+            }
+            const Ray32 r32 = ray32(o, dd, kp.bvh_rbox);
+            bool more = true;
+#pragma unroll 1
+            for (int j = 0; j < QB; ++j) {
+                if (more) {
+                    Cnt cnt;
+                    more = bvh_step<false, false>(kp, o, dd, r32, stk0 + ow, node, sp, best, kind, win, win_orig, cnt);
+                }
+                if (__ballot(more) == 0ull) break;
+            }
+            best_lds[ow] = best;
+            wst_lds[256 + ow] = win;
+            wst_lds[512 + ow] = win_orig;
+            wst_lds[ow] = node | (sp << 16) | (kind << 24) | (more ? 0 : QC_DONE);
+        }
+        __syncthreads();
     }
-    if (kp.trace) {                  // diagnostics (RT_QUEUE_TRACE): per lane start, end, rounds, tasks
-        unsigned long long* q = kp.trace + ((size_t)blockIdx.x * 256 + threadIdx.x) * RT_TRACE_WORDS;
-        q[0] = (unsigned long long)t_start;
-        q[1] = (unsigned long long)wall_clock64();
-        q[2] = rounds;
-        q[3] = ntasks;
-#if RT_QSTATS
-        for (int j = 0; j < 14; ++j) q[4 + j] = qs[j];
-#endif
-    }
+    Q.trace_out(kp, t_start, rounds);
 }
 #endif
 
@@ -2774,14 +2890,6 @@ static void launch_variant(const KParams& kp_in, void* stream)
     const dim3 g = grid_for(kp_in);
     const hipStream_t st = (hipStream_t)stream;
     KParams kp = kp_in;
-#if RT_QSTATS
-    // diagnostic build: samples_coop's census summed into 16 counters, appended to RT_QUEUE_TRACE
-    const char* tf = COUNT ? nullptr : std::getenv("RT_QUEUE_TRACE");
-    if (tf && kp.bvh) {
-        (void)hipMalloc((void**)&kp.trace, 16 * sizeof(unsigned long long));
-        (void)hipMemsetAsync(kp.trace, 0, 16 * sizeof(unsigned long long), st);
-    }
-#endif
     if (!COUNT && kp.f32) {
         if (kp.bvh && kp.sky) hipLaunchKernelGGL((render_kernel_f32<true, true>), g, dim3(256), 0, st, kp);
         else if (kp.bvh) hipLaunchKernelGGL((render_kernel_f32<true, false>), g, dim3(256), 0, st, kp);
@@ -2793,18 +2901,6 @@ static void launch_variant(const KParams& kp_in, void* stream)
     else if (kp.bvh) hipLaunchKernelGGL((render_kernel<COUNT, true, false>), g, dim3(256), 0, st, kp);
     else if (kp.sky) hipLaunchKernelGGL((render_kernel<COUNT, false, true>), g, dim3(256), 0, st, kp);
     else hipLaunchKernelGGL((render_kernel<COUNT, false, false>), g, dim3(256), 0, st, kp);
-#if RT_QSTATS
-    if (kp.trace) {
-        unsigned long long h[16];
-        (void)hipStreamSynchronize(st);
-        (void)hipMemcpy(h, kp.trace, sizeof h, hipMemcpyDeviceToHost);
-        (void)hipFree(kp.trace);
-        if (FILE* f = std::fopen(tf, "ab")) {
-            std::fwrite(h, sizeof(unsigned long long), 16, f);
-            std::fclose(f);
-        }
-    }
-#endif
 }
 
 #if RT_QUEUE > 0
@@ -2813,31 +2909,44 @@ static void queue_occupancy(int& nb)
 {
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<SKY, AOM, QB>, 256, 0);
 }
+template <bool SKY, int AOM, int QB>
+static void queue_occupancy_c(int& nb)
+{
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_qc<SKY, AOM, QB>, 256, 0);
+}
 
 // Resident blocks of the queue kernel on this device (grid of render_kernel_q).
 // Cached per device and variant; rt_fill_canva may run on several host
 // threads at once (main.c's pthreads), so the cache is atomic (every thread
 // computes the same value).
 template <int QB>
-static void queue_occupancy_v(bool sky, bool ao, int& nb)
+static void queue_occupancy_v(bool sky, bool ao, bool qc, int& nb)
 {
+    if (qc && QB > 0) {
+        if (sky && ao) queue_occupancy_c<true, AO_ON, QB>(nb);
+        else if (sky) queue_occupancy_c<true, AO_OFF, QB>(nb);
+        else if (ao) queue_occupancy_c<false, AO_ON, QB>(nb);
+        else queue_occupancy_c<false, AO_OFF, QB>(nb);
+        return;
+    }
     if (sky && ao) queue_occupancy<true, AO_ON, QB>(nb);
     else if (sky) queue_occupancy<true, AO_OFF, QB>(nb);
     else if (ao) queue_occupancy<false, AO_ON, QB>(nb);
     else queue_occupancy<false, AO_OFF, QB>(nb);
 }
-static unsigned queue_grid(bool sky, bool ao, int qb)
+static unsigned queue_grid(bool sky, bool ao, int qb, bool qc)
 {
-    static std::atomic<int> cached[12][64];
+    static std::atomic<int> cached[24][64];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? 1 : 2)][dev & 63];
+    std::atomic<int>& slot =
+        cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? 1 : 2) + (qc ? 12 : 0)][dev & 63];
     int c = slot.load(std::memory_order_relaxed);
     if (c <= 0) {
         int nb = 0, ncu = 0;
-        if (qb == 0) queue_occupancy_v<0>(sky, ao, nb);
-        else if (qb == 3) queue_occupancy_v<3>(sky, ao, nb);
-        else queue_occupancy_v<4>(sky, ao, nb);
+        if (qb == 0) queue_occupancy_v<0>(sky, ao, qc, nb);
+        else if (qb == 3) queue_occupancy_v<3>(sky, ao, qc, nb);
+        else queue_occupancy_v<4>(sky, ao, qc, nb);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         c = std::max(1, nb) * std::max(1, ncu);
         if (std::getenv("RT_QUEUE_VERBOSE")) std::fprintf(stderr, "render_kernel_q: %d blocks/CU x %d CUs -> %d\n", nb, ncu, c);
@@ -2850,8 +2959,15 @@ static unsigned queue_grid(bool sky, bool ao, int qb)
 }
 
 template <int QB>
-static void queue_launch(bool sky, bool ao, unsigned nb, hipStream_t st, const KParams& k2)
+static void queue_launch(bool sky, bool ao, bool qc, unsigned nb, hipStream_t st, const KParams& k2)
 {
+    if (qc && QB > 0) {
+        if (sky && ao) hipLaunchKernelGGL((render_kernel_qc<true, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
+        else if (sky) hipLaunchKernelGGL((render_kernel_qc<true, AO_OFF, QB>), dim3(nb), dim3(256), 0, st, k2);
+        else if (ao) hipLaunchKernelGGL((render_kernel_qc<false, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
+        else hipLaunchKernelGGL((render_kernel_qc<false, AO_OFF, QB>), dim3(nb), dim3(256), 0, st, k2);
+        return;
+    }
     if (sky && ao) hipLaunchKernelGGL((render_kernel_q<true, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
     else if (sky) hipLaunchKernelGGL((render_kernel_q<true, AO_OFF, QB>), dim3(nb), dim3(256), 0, st, k2);
     else if (ao) hipLaunchKernelGGL((render_kernel_q<false, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
@@ -2873,7 +2989,11 @@ int launch_render(const KParams& kp, void* stream)
         // node visits per lane and round: 4 for shallow trees, 3 for deep ones
         // (kp.bvh_steps, host; compile-time per instantiation)
         const int qb = qbvh ? (kp.bvh_steps <= 3 ? 3 : 4) : 0;
-        const unsigned nb = queue_grid(sky, ao, qb);
+        // BVH scenes: closest hits compacted over the block (render_kernel_qc);
+        // RT_QC=0 selects render_kernel_q's per-lane walks (A/B)
+        static const bool qc_env = !(std::getenv("RT_QC") && std::atoi(std::getenv("RT_QC")) == 0);
+        const bool qc = qb > 0 && qc_env;
+        const unsigned nb = queue_grid(sky, ao, qb, qc);
         unsigned long long* tr = nullptr;
         const char* tf = std::getenv("RT_QUEUE_TRACE");
         if (tf) (void)hipMalloc((void**)&tr, (size_t)nb * 256 * RT_TRACE_WORDS * sizeof(unsigned long long));
@@ -2887,9 +3007,9 @@ int launch_render(const KParams& kp, void* stream)
         // chunk starts c*S/P in 32 bits when (P + 1) * S fits
         k2.qm_chunks = (unsigned long long)(kp.chunk_den + 1) * (unsigned long long)kp.S < (1ull << 32)
                            ? qdiv_magic(kp.chunk_den) : 0u;
-        if (qb == 3) queue_launch<3>(sky, ao, nb, st, k2);
-        else if (qb == 4) queue_launch<4>(sky, ao, nb, st, k2);
-        else queue_launch<0>(sky, ao, nb, st, k2);
+        if (qb == 3) queue_launch<3>(sky, ao, qc, nb, st, k2);
+        else if (qb == 4) queue_launch<4>(sky, ao, qc, nb, st, k2);
+        else queue_launch<0>(sky, ao, qc, nb, st, k2);
         if (tr) {
             std::vector<unsigned long long> h((size_t)nb * 256 * RT_TRACE_WORDS);
             (void)hipStreamSynchronize(st);

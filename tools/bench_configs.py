@@ -8,8 +8,10 @@ rows §8(f-2) acceleration targets) and C5's 4K frame (3840x2880, C3 scene;
 `full_frame_s_on_config_gpus_linear` divides by the config's GPU count,
 which the row tiling achieves up to the gather).  Full frames at a reduced spp
 (Msamples/s is spp-independent: pixels are independent and the per-sample
-work does not depend on S); kernel time from HIP events on the launch
-stream, events/sample from rt_count_async at 4 spp.
+work does not depend on S); spp_chunks RT_SPP_CHUNKS_AUTO as bench.py (so
+--spp sets the task size: S/32 samples per slice from 32 spp on); kernel
+time from HIP events on the launch stream, events/sample from rt_count_async
+at 4 spp.
 """
 import argparse
 import json
@@ -37,9 +39,9 @@ CONFIGS = {
 }
 
 
-def run(name, spp_scale, dev, stream):
+def run(name, spp_scale, dev, stream, spp_override=0):
     mesh_fn, spp, bounces, ao, ao_int, full_spp, W, H, gpus = CONFIGS[name]
-    spp = max(1, int(spp * spp_scale))
+    spp = spp_override or max(1, int(spp * spp_scale))
     spheres = scenes.cornell_spheres()
     if mesh_fn == "sweep":
         spheres, (tris, qm, mats, tw, th, nm) = scenes.synthetic_cornell(10, 100)
@@ -53,7 +55,7 @@ def run(name, spp_scale, dev, stream):
         scene = tipe_rt.make_scene(spheres, tris, qm, mats, tw, th, nm)
         nt = len(tris)
     cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
-    p = tipe_rt.make_params(W, H, spp, bounces, cam, focus=3.0, use_ao=ao, ao=ao_int, chunks=min(8, spp))
+    p = tipe_rt.make_params(W, H, spp, bounces, cam, focus=3.0, use_ao=ao, ao=ao_int, chunks=tipe_rt.RT_SPP_CHUNKS_AUTO)
     ds = tipe_rt.DeviceScene(scene, dev.index)
     tiling = tipe_rt.band_tiling(0, H - 1)
     out = torch.empty((3, H, W, 3), dtype=torch.float64, device=dev)
@@ -95,12 +97,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--spp-scale", type=float, default=1.0)
     ap.add_argument("--only", default=",".join(CONFIGS))
+    ap.add_argument("--spp", type=int, default=0, help="spp of every config (default: the table's, x --spp-scale)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
     for name in args.only.split(","):
-        print(json.dumps(run(name, args.spp_scale, dev, stream)), flush=True)
+        print(json.dumps(run(name, args.spp_scale, dev, stream, args.spp)), flush=True)
 
 
 if __name__ == "__main__":
