@@ -328,9 +328,13 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             const double r0 = __builtin_amdgcn_rsq(D);
             const double tt = D * r0;
             const double sa = fma(tt * 0.5, fma(-tt, r0, 1.0), tt);
-            const double n1 = -h - sa, n2 = sa - h;
+            const double n1 = -h - sa;
             const bool r1 = n1 >= thrM;                     // n1 may reach 1e-4: hit_sphere takes t1
-            const double n = r1 ? n1 : n2;
+            // the chosen root: n1 = -h - sa, or n2 = -h + sa; in the sphere-scene queue
+            // kernel (AMGM) as one fma with a selected sign (s * sa is exact; C2
+            // +0.7 %), elsewhere a select (the fma's constants cost the BVH
+            // instantiations registers: sweep -1.4 %)
+            const double n = AMGM ? fma(r1 ? -1.0 : 1.0, sa, -h) : (r1 ? n1 : sa - h);
             const double tP = CU ? (r1 ? thrP : thrP2) : thrP, tM = CU ? (r1 ? thrM : thrM2) : thrM;
             const bool sure = n >= tP;
             amb = amb || (valid && (sure != (n >= tM)));    // the chosen root straddles 1e-4
@@ -2258,200 +2262,6 @@ struct QPath {
     }
 };
 
-// One lane of the queue kernels outside its path: the task it runs (chunk,
-// pixel of the band), the wave's batch of tasks and the draw stream of the
-// sample in flight.  take_tasks and next_ray are steps 3 and 4 of a round of
-// render_kernel_q and render_kernel_qc.
-template <bool SKY, int AOM>
-struct QLane {
-    QPath<SKY, AOM> L;
-    Stream st;                       // draws of the sample in flight (next31 for refraction / AO)
-    int x, g, s1;
-    unsigned chunk, p, pixel;
-    unsigned qb, qe;                 // the wave's batch of tasks [qb, qe) (wave-uniform)
-    unsigned ntasks;
-    bool owns;                       // the lane's LDS sums belong to task (chunk, p)
-
-    __device__ __forceinline__ void init(const KParams& kp, uint32_t* rng)
-    {
-        L.o = L.d = L.cd = L.inc = L.rc = v3(0, 0, 0);
-        L.top_n2 = 1.0;
-        L.best = 0.0;
-        L.i = 0; L.kind = HIT_NONE; L.win = -1; L.s = 0;
-        L.chain = true; L.ao_cast = false;
-        L.state = SM_CAM;            // s = 0 >= s1 = 0: takes a task first
-        x = g = s1 = 0;
-        chunk = p = pixel = 0;
-        qb = qe = 0;
-        ntasks = 0;
-        owns = false;
-        st.start(0u, 0u, kp.key0, kp.key1, rng);
-    }
-
-    // ---- 3. lanes whose task is done take the next one ----------------------
-    // Tasks come from a per-launch counter, RT_QUEUE per atomic: the wave
-    // takes a batch and hands its tasks to its lanes as they need them.
-    __device__ __forceinline__ void take_tasks(double* acc, int lane)
-    {
-        const bool need = L.state == SM_CAM && L.s >= s1;
-        const unsigned long long nm = __ballot(need);
-        if (!nm) return;             // wave-uniform
-        // launch constants re-read here (SMEM) instead of living in SGPRs
-        // spilled to VGPR lanes across the whole round
-        const KParamsK K = kp_here();
-        unsigned t = 0;
-        const unsigned nn = (unsigned)__popcll(nm), avail = qe - qb;
-        const unsigned rank = (unsigned)__popcll(nm & ((1ull << lane) - 1ull));
-        if (avail < nn) {            // a new batch (nn <= 64 <= RT_QUEUE): old tasks first
-            unsigned nb = 0;
-            if (lane == __ffsll((long long)nm) - 1) nb = atomicAdd(K->task_ctr, (unsigned)RT_QUEUE);
-            nb = __shfl(nb, __ffsll((long long)nm) - 1, 64);
-            t = rank < avail ? qb + rank : nb + (rank - avail);
-            qb = nb + (nn - avail);
-            qe = nb + RT_QUEUE;
-        } else {
-            t = qb + rank;
-            qb += nn;
-        }
-        if (!need) return;
-        ++ntasks;
-        if (owns) {                  // task done: its sums to the chunk partials
-            double* q = K->partial + ((size_t)chunk * ((unsigned)K->band_rows * (unsigned)K->W) + p) * 9;
-#pragma unroll
-            for (int j = 0; j < 9; ++j) q[j] = acc[j * 256];
-            owns = false;
-        }
-        if (t >= K->npx_here * (unsigned)K->chunks) {
-            L.state = SM_DONE;
-            return;
-        }
-        // task t = (chunk, pixel p of the band): launch-constant divisors
-        chunk = udiv_q(t, K->npx_here, K->qm_npx, p);
-        unsigned xr;
-        const unsigned row = udiv_q(p, (unsigned)K->W, K->qm_w, xr);
-        const int ly = K->band_y0 + (int)row;
-        x = (int)xr;
-        bool valid = ly < K->local_rows;
-        if (valid) {
-            unsigned yy;
-            const int lt = (int)udiv_q((unsigned)ly, (unsigned)K->tile_rows, K->qm_tile, yy);
-            g = K->row_base + (K->tile_first + lt * K->tile_step) * K->tile_rows + (int)yy;
-            valid = g < K->row_end;
-        }
-        if (valid) {                 // otherwise the lane takes its next task next round
-            pixel = (uint32_t)g * (uint32_t)K->W + (uint32_t)x;
-            L.s = chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk);
-            s1 = chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk + 1u);
-#pragma unroll
-            for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
-            owns = true;
-        }
-    }
-
-    // tracer with nbRebondMax <= 0 returns (0, 0, 0) albedo/normal/colour:
-    // one sample of the task; false when the lane has no such sample
-    __device__ __forceinline__ bool empty_sample(const KParams& kp, double* acc)
-    {
-        if (!(kp.B <= 0 && L.state == SM_CAM && L.s < s1)) return false;
-        acc_add(acc, ACC_ALB, v3(0, 0, 0));
-        acc_add(acc, ACC_NRM, v3(0, 0, 0));
-        acc_add(acc, ACC_RAD, v3(0, 0, 0));
-        ++L.s;
-        return true;
-    }
-
-    // ---- 4. next ray: bounce direction or camera ray (shared work) --------
-    __device__ __forceinline__ void next_ray(const KParams& kp, int role, const QHit& H, double* acc, uint32_t* rng)
-    {
-        if (role == ROLE_NONE) return;
-        const bool cam = role == ROLE_CAMERA;
-        // draws: a bounce uses draws n, n+1 of its sample (rtutility.h:
-        // 189-203); a camera ray draws 0-3 of sample s (main.c:265-269)
-        const uint32_t nd = cam ? 0u : st.n;
-        const uint32_t sa = nd & 3u, sb = (nd + 1u) & 3u;
-        uint32_t wa = 0, wb = 0;
-        if (!cam && sa != 0u) wa = rng[sa * 256];          // cached word of the current block
-        if (!cam && sb != 0u && sa != 0u) wb = rng[sb * 256];
-        Philox blk{0, 0, 0, 0};
-        if (cam || sa == 0u || sb == 0u) {                 // a new block: one Philox for both roles
-            const uint32_t bi = cam ? 0u : ((nd + (sa == 0u ? 0u : 1u)) >> 2);
-            blk = philox4x32_10(bi, 0u, pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1);
-            if (!cam) {                                     // keep the rest of the block
-                rng[256] = blk.w1;
-                rng[512] = blk.w2;
-                rng[768] = blk.w3;
-            }
-        }
-        if (!cam) {
-            if (sa == 0u) wa = blk.w0;
-            if (sb == 0u) wb = blk.w0;
-            else if (sa == 0u) wb = blk.w1;
-        }
-        V3 X;
-        V3 no = v3(0, 0, 0);
-        if (cam) {
-            CamDraws w{blk, 0};
-            const double ju = -0.5 + 1.0 * unit31(w.next31());     // randomDouble(-0.5, 0.5)
-            const double jv = -0.5 + 1.0 * unit31(w.next31());
-            const int b = opq0();
-            const cdptr U = (cdptr)kp.uni;
-            const double nu = (double)x + ju, nv = (double)g + jv;
-            const double rcw = U[b + U_RC_WM1], rch = U[b + U_RC_HM1];
-            const double u = rcw != 0.0 ? div_core(nu, U[b + U_WM1], rcw) : nu / U[b + U_WM1];
-            const double v = rch != 0.0 ? div_core(nv, U[b + U_HM1], rch) : nv / U[b + U_HM1];
-            const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
-            const V3 ch = v3(U[b + U_CAM_H], U[b + U_CAM_H + 1], U[b + U_CAM_H + 2]);
-            const V3 cv = v3(U[b + U_CAM_V], U[b + U_CAM_V + 1], U[b + U_CAM_V + 2]);
-            const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
-            const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));     // get_ray, camera.h:42-55
-            const V3 dest = co + muls(dir, U[b + U_FOCUS]);
-            if (kp.cam_pin) {                              // zero aperture: the origin itself (host-checked)
-                no = co;
-            } else {
-                const double jx = -0.5 + 1.0 * unit31(w.next31());
-                const double jy = -0.5 + 1.0 * unit31(w.next31());
-                const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
-                no = co + v3(dx, dy, 0);
-            }
-            X = dest - no;
-        } else {
-            // random_dir_no_norm (rtutility.h:189-203), then n + dir (main.c:163)
-            const double u = unit31(wa >> 1);
-            const double v = unit31(wb >> 1);
-            X = H.hn + normalize_unit(sampler_vec(u, v));
-            st.n += 2;
-        }
-        const V3 dn = normalize(X);
-        if (cam) {                                         // the new sample's primary ray
-            L.o = no;
-            L.d = dn;
-            if (AOM == AO_ON) L.cd = dn;
-            L.inc = v3(0, 0, 0);
-            L.rc = v3(1, 1, 1);
-            L.top_n2 = 1.0;
-            L.i = 0;
-            L.chain = true;
-            L.ao_cast = false;
-            L.state = SM_CAST;
-            st.start(pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1, rng);
-            st.n = 4;                                      // draws 0-3 were the camera's
-        } else {
-            L.finish_bounce(kp, dn, st, acc, H);
-        }
-    }
-
-    // per lane start, end, rounds, tasks (RT_QUEUE_TRACE diagnostics)
-    __device__ __forceinline__ void trace_out(const KParams& kp, long long t_start, unsigned rounds) const
-    {
-        if (!kp.trace) return;
-        unsigned long long* q = kp.trace + ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
-        q[0] = (unsigned long long)t_start;
-        q[1] = (unsigned long long)wall_clock64();
-        q[2] = rounds;
-        q[3] = ntasks;
-    }
-};
-
 template <bool SKY, int AOM, int QB>
 __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
 {
@@ -2460,10 +2270,20 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     double* acc = acc_lds + threadIdx.x;
     uint32_t* rng = rng_lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
-    QLane<SKY, AOM> Q;
-    Q.init(kp, rng);
-    QPath<SKY, AOM>& L = Q.L;
+    unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
+    QPath<SKY, AOM> L;
+    L.o = L.d = L.cd = L.inc = L.rc = v3(0, 0, 0);
+    L.top_n2 = 1.0;
+    L.best = 0.0;
+    L.i = 0; L.kind = HIT_NONE; L.win = -1; L.s = 0;
+    L.chain = true; L.ao_cast = false;
+    L.state = SM_CAM;                // s = 0 >= s1 = 0: takes a task first
+    int x = 0, g = 0, s1 = 0;
     int node = 0, sp = 0, win_orig = 0;      // BVH walk in flight (state SM_TRAV)
+    unsigned chunk = 0, p = 0, pixel = 0;
+    bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
+    Stream st;                       // draw stream of the sample in flight (next31 for refraction / AO)
+    st.start(0u, 0u, kp.key0, kp.key1, rng);
     // shallow trees (QB 4: depth4 <= 4, e.g. the 50-node sweep tree) keep
     // their top nodes in LDS: sweep +5.7 %; deep ones gain nothing (C4 -0.5 %)
     constexpr int NTOP = QB == 4 ? RT_QB_TOP : 0;
@@ -2475,7 +2295,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
         __syncthreads();
     }
     const long long t_start = kp.trace ? wall_clock64() : 0;
-    unsigned rounds = 0;
+    unsigned rounds = 0, ntasks = 0;
     while (true) {
         ++rounds;
         // ---- 1. closest hit (main.c:52-92) for every lane with a ray ------
@@ -2522,180 +2342,156 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
         H.refr = H.hole = false;
         if (L.state == SM_RESOLVE) role = L.resolve_hit(kp, acc, H);
         // ---- 3. lanes whose task is done take the next one -----------------
-        Q.take_tasks(acc, lane);
-        if (__ballot(L.state != SM_DONE) == 0ull) break;     // every lane of the wave is done
-        if (Q.empty_sample(kp, acc)) continue;
-        if (L.state == SM_CAM && L.s < Q.s1) role = ROLE_CAMERA;
-        // ---- 4. next ray: bounce direction or camera ray (shared work) ----
-        Q.next_ray(kp, role, H, acc, rng);
-    }
-    Q.trace_out(kp, t_start, rounds);
-}
-
-// ---- BVH scenes: closest hits compacted over the block (render_kernel_qc) --
-// In render_kernel_q<.., QB> a lane whose ray walks the tree spends whole
-// rounds in SM_TRAV while its wave runs the other lanes' path work, and the
-// walks themselves run with the wave's other lanes idle (C4: lane
-// utilisation 0.35).  Here the closest hit of every cast (main.c:52-92: the
-// sphere candidate pass, then up to QB node visits of the triangle BVH) is
-// taken out of the owner lane: each round
-//   A. (each wave, its own lanes) a finished cast's hit goes back to its
-//      owner, which shades it, takes tasks and makes its next ray (the same
-//      QPath / QLane steps as render_kernel_q), then posts the ray: o and the
-//      cast direction into the owner's LDS slot, the owner's id into its
-//      wave's list;
-//   B. block barrier;
-//   C. the block's posted casts -- new ones and walks in flight -- are dealt
-//      densely over its 256 threads (item i to thread (i + 64 r) mod 256, the
-//      start wave r rotating by round and block so no SIMD always gets the
-//      remainder); a thread runs its item's sphere pass if the cast is new
-//      and up to QB node visits, and stores the walk state (node, stack
-//      pointer, best, winner) back into the owner's slot; the stack stays the
-//      owner's LDS column;
-//   D. block barrier.
-// Every cast is the same closest_hit arithmetic, only run by another lane of
-// the block, so frames are bit-identical to render_kernel_q's.  Waves whose
-// lanes are all done keep looping as tracers until the whole block is done
-// (the loop exit is block-uniform, so every wave reaches every barrier).
-// LDS 52 KiB per block (sums, Philox cache, stacks, ray slots): 3 blocks per CU.
-#ifndef RT_WAVES_PER_SIMD_QC
-#define RT_WAVES_PER_SIMD_QC 3
-#endif
-template <bool SKY, int AOM, int QB>
-__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_QC) void render_kernel_qc(const KParams kp)
-{
-    __shared__ double acc_lds[ACC_SLOTS * 256];
-    __shared__ uint32_t rng_lds[4 * 256];
-    __shared__ double ray_lds[6 * 256];          // owner t's cast: o.x o.y o.z d.x d.y d.z at [k * 256 + t]
-    __shared__ double best_lds[256];             // its closest t so far
-    __shared__ int wst_lds[3 * 256];             // [t] node | sp << 16 | kind << 24 | QC_NEW | QC_DONE;
-                                                 // [256 + t] winner; [512 + t] winner's caller index
-    __shared__ unsigned short list_lds[256];     // wave w's posted owners at [64 w, 64 w + n_w)
-    __shared__ int wave_lds[8];                  // [w] n_w; [4 + w] wave w has lanes with work
-    constexpr int QC_NEW = 1 << 26, QC_DONE = 1 << 27;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    double* acc = acc_lds + tid;
-    uint32_t* rng = rng_lds + tid;
-    unsigned short* stk0 = bvh_stack_q() - tid;  // column c: stk0 + c
-    QLane<SKY, AOM> Q;
-    Q.init(kp, rng);
-    QPath<SKY, AOM>& L = Q.L;
-    unsigned rot = blockIdx.x & 3u;
-    const long long t_start = kp.trace ? wall_clock64() : 0;
-    unsigned rounds = 0;
-    while (true) {
-        ++rounds;
-        // ---- A. owner phase --------------------------------------------------
-        if (L.state == SM_TRAV) {                // a posted cast: done in the last C phase?
-            const int w0 = wst_lds[tid];
-            if (w0 & QC_DONE) {
-                L.best = best_lds[tid];
-                L.kind = (w0 >> 24) & 3;
-                L.win = wst_lds[256 + tid];
-                L.state = SM_RESOLVE;
+        const bool need = L.state == SM_CAM && L.s >= s1;
+        const unsigned long long nm = __ballot(need);
+        if (nm) {                    // wave-uniform: tasks for the lanes that need one
+            // launch constants re-read here (SMEM) instead of living in SGPRs
+            // spilled to VGPR lanes across the whole round
+            const KParamsK K = kp_here();
+            unsigned t = 0;
+            const unsigned nn = (unsigned)__popcll(nm), avail = qe - qb;
+            const unsigned rank = (unsigned)__popcll(nm & ((1ull << lane) - 1ull));
+            if (avail < nn) {        // a new batch (nn <= 64 <= RT_QUEUE): old tasks first
+                unsigned nb = 0;
+                if (lane == __ffsll((long long)nm) - 1) nb = atomicAdd(K->task_ctr, (unsigned)RT_QUEUE);
+                nb = __shfl(nb, __ffsll((long long)nm) - 1, 64);
+                t = rank < avail ? qb + rank : nb + (rank - avail);
+                qb = nb + (nn - avail);
+                qe = nb + RT_QUEUE;
+            } else {
+                t = qb + rank;
+                qb += nn;
             }
-        }
-        int role = ROLE_NONE;
-        QHit H;
-        H.hn = v3(0, 0, 0);
-        H.rs = 0.0;
-        H.refr = H.hole = false;
-        if (L.state == SM_RESOLVE) role = L.resolve_hit(kp, acc, H);
-        Q.take_tasks(acc, lane);
-        if (!Q.empty_sample(kp, acc)) {
-            if (L.state == SM_CAM && L.s < Q.s1) role = ROLE_CAMERA;
-            Q.next_ray(kp, role, H, acc, rng);
-        }
-        if (L.state == SM_CAST) {                // post the cast
-            const V3 dd = L.cast_dir();
-            ray_lds[tid] = L.o.x;
-            ray_lds[256 + tid] = L.o.y;
-            ray_lds[512 + tid] = L.o.z;
-            ray_lds[768 + tid] = dd.x;
-            ray_lds[1024 + tid] = dd.y;
-            ray_lds[1280 + tid] = dd.z;
-            wst_lds[tid] = QC_NEW;
-            L.state = SM_TRAV;
-        }
-        // wave w's new casts at list [64 w, 64 w + n_w), its walks in flight
-        // from 64 w + 63 down: the block's items are all new casts first (their
-        // sphere pass then runs on whole waves), then the walks
-        const bool fresh = L.state == SM_TRAV && wst_lds[tid] == QC_NEW;
-        const bool cont = L.state == SM_TRAV && !fresh;
-        const unsigned long long fm = __ballot(fresh), cm = __ballot(cont);
-        const unsigned long long below = (1ull << lane) - 1ull;
-        if (fresh) list_lds[wave * 64 + __popcll(fm & below)] = (unsigned short)tid;
-        if (cont) list_lds[wave * 64 + 63 - __popcll(cm & below)] = (unsigned short)tid;
-        const unsigned long long live = __ballot(L.state != SM_DONE);
-        if (lane == 0) {
-            wave_lds[wave] = __popcll(fm) | (__popcll(cm) << 8);
-            wave_lds[4 + wave] = live != 0ull;
-        }
-        __syncthreads();
-        // ---- C. tracer phase: the block's casts over its threads -------------
-        if ((wave_lds[4] | wave_lds[5] | wave_lds[6] | wave_lds[7]) == 0) break;   // block-uniform
-        const int v0 = wave_lds[0], v1 = wave_lds[1], v2 = wave_lds[2], v3_ = wave_lds[3];
-        const int f0 = v0 & 255, f1 = v1 & 255, f2 = v2 & 255, f3 = v3_ & 255;
-        const int nf = f0 + f1 + f2 + f3;
-        const int n_items = nf + (v0 >> 8) + (v1 >> 8) + (v2 >> 8) + (v3_ >> 8);
-        const int it = (tid - 64 * (int)rot) & 255;
-        rot = (rot + 1u) & 3u;
-        if (it < n_items) {
-            // item it: the it-th new cast, else the (it - nf)-th walk, in wave order
-            const bool isnew = it < nf;
-            const int c0 = isnew ? f0 : v0 >> 8, c1 = isnew ? f1 : v1 >> 8, c2 = isnew ? f2 : v2 >> 8;
-            int k = isnew ? it : it - nf, w = 0;
-            if (k >= c0) {
-                k -= c0;
-                w = 1;
-                if (k >= c1) {
-                    k -= c1;
-                    w = 2;
-                    if (k >= c2) {
-                        k -= c2;
-                        w = 3;
+            if (need) {
+                ++ntasks;
+                if (owns) {          // task done: its sums to the chunk partials
+                    double* q = K->partial + ((size_t)chunk * ((unsigned)K->band_rows * (unsigned)K->W) + p) * 9;
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) q[j] = acc[j * 256];
+                    owns = false;
+                }
+                if (t >= K->npx_here * (unsigned)K->chunks) {
+                    L.state = SM_DONE;
+                } else {
+                    // task t = (chunk, pixel p of the band): launch-constant divisors
+                    chunk = udiv_q(t, K->npx_here, K->qm_npx, p);
+                    unsigned xr;
+                    const unsigned row = udiv_q(p, (unsigned)K->W, K->qm_w, xr);
+                    const int ly = K->band_y0 + (int)row;
+                    x = (int)xr;
+                    bool valid = ly < K->local_rows;
+                    if (valid) {
+                        unsigned yy;
+                        const int lt = (int)udiv_q((unsigned)ly, (unsigned)K->tile_rows, K->qm_tile, yy);
+                        g = K->row_base + (K->tile_first + lt * K->tile_step) * K->tile_rows + (int)yy;
+                        valid = g < K->row_end;
+                    }
+                    if (valid) {     // otherwise the lane takes its next task next round
+                        pixel = (uint32_t)g * (uint32_t)K->W + (uint32_t)x;
+                        L.s = chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk);
+                        s1 = chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk + 1u);
+#pragma unroll
+                        for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
+                        owns = true;
                     }
                 }
             }
-            const int ow = list_lds[isnew ? w * 64 + k : w * 64 + 63 - k];
-            const V3 o = v3(ray_lds[ow], ray_lds[256 + ow], ray_lds[512 + ow]);
-            const V3 dd = v3(ray_lds[768 + ow], ray_lds[1024 + ow], ray_lds[1280 + ow]);
-            const int w0 = wst_lds[ow];
-            double best;
-            int kind, win, win_orig, node, sp;
-            if (w0 & QC_NEW) {                   // spheres first (main.c:59-78)
-                Cnt cnt;
-                win = cast_spheres<false, false>(kp, o, dd, best, cnt);
-                kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
-                win_orig = 0;
-                node = 0;
-                sp = 0;
-            } else {
-                best = best_lds[ow];
-                kind = (w0 >> 24) & 3;
-                win = wst_lds[256 + ow];
-                win_orig = wst_lds[512 + ow];
-                node = w0 & 0xffff;
-                sp = (w0 >> 16) & 0xff;
-            }
-            const Ray32 r32 = ray32(o, dd, kp.bvh_rbox);
-            bool more = true;
-#pragma unroll 1
-            for (int j = 0; j < QB; ++j) {
-                if (more) {
-                    Cnt cnt;
-                    more = bvh_step<false, false>(kp, o, dd, r32, stk0 + ow, node, sp, best, kind, win, win_orig, cnt);
-                }
-                if (__ballot(more) == 0ull) break;
-            }
-            best_lds[ow] = best;
-            wst_lds[256 + ow] = win;
-            wst_lds[512 + ow] = win_orig;
-            wst_lds[ow] = node | (sp << 16) | (kind << 24) | (more ? 0 : QC_DONE);
         }
-        __syncthreads();
+        if (__ballot(L.state != SM_DONE) == 0ull) break;     // every lane of the wave is done
+        // tracer with nbRebondMax <= 0 returns (0, 0, 0) albedo/normal/colour
+        if (kp.B <= 0 && L.state == SM_CAM && L.s < s1) {
+            acc_add(acc, ACC_ALB, v3(0, 0, 0));
+            acc_add(acc, ACC_NRM, v3(0, 0, 0));
+            acc_add(acc, ACC_RAD, v3(0, 0, 0));
+            ++L.s;
+            continue;
+        }
+        if (L.state == SM_CAM && L.s < s1) role = ROLE_CAMERA;
+        // ---- 4. next ray: bounce direction or camera ray (shared work) ----
+        if (role != ROLE_NONE) {
+            const bool cam = role == ROLE_CAMERA;
+            // draws: a bounce uses draws n, n+1 of its sample (rtutility.h:
+            // 189-203); a camera ray draws 0-3 of sample s (main.c:265-269)
+            const uint32_t nd = cam ? 0u : st.n;
+            const uint32_t sa = nd & 3u, sb = (nd + 1u) & 3u;
+            uint32_t wa = 0, wb = 0;
+            if (!cam && sa != 0u) wa = rng[sa * 256];          // cached word of the current block
+            if (!cam && sb != 0u && sa != 0u) wb = rng[sb * 256];
+            Philox blk{0, 0, 0, 0};
+            if (cam || sa == 0u || sb == 0u) {                 // a new block: one Philox for both roles
+                const uint32_t bi = cam ? 0u : ((nd + (sa == 0u ? 0u : 1u)) >> 2);
+                blk = philox4x32_10(bi, 0u, pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1);
+                if (!cam) {                                     // keep the rest of the block
+                    rng[256] = blk.w1;
+                    rng[512] = blk.w2;
+                    rng[768] = blk.w3;
+                }
+            }
+            if (!cam) {
+                if (sa == 0u) wa = blk.w0;
+                if (sb == 0u) wb = blk.w0;
+                else if (sa == 0u) wb = blk.w1;
+            }
+            V3 X;
+            V3 no = v3(0, 0, 0);
+            if (cam) {
+                CamDraws w{blk, 0};
+                const double ju = -0.5 + 1.0 * unit31(w.next31());     // randomDouble(-0.5, 0.5)
+                const double jv = -0.5 + 1.0 * unit31(w.next31());
+                const int b = opq0();
+                const cdptr U = (cdptr)kp.uni;
+                const double nu = (double)x + ju, nv = (double)g + jv;
+                const double rcw = U[b + U_RC_WM1], rch = U[b + U_RC_HM1];
+                const double u = rcw != 0.0 ? div_core(nu, U[b + U_WM1], rcw) : nu / U[b + U_WM1];
+                const double v = rch != 0.0 ? div_core(nv, U[b + U_HM1], rch) : nv / U[b + U_HM1];
+                const V3 co = v3(U[b + U_CAM_O], U[b + U_CAM_O + 1], U[b + U_CAM_O + 2]);
+                const V3 ch = v3(U[b + U_CAM_H], U[b + U_CAM_H + 1], U[b + U_CAM_H + 2]);
+                const V3 cv = v3(U[b + U_CAM_V], U[b + U_CAM_V + 1], U[b + U_CAM_V + 2]);
+                const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
+                const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));     // get_ray, camera.h:42-55
+                const V3 dest = co + muls(dir, U[b + U_FOCUS]);
+                if (kp.cam_pin) {                              // zero aperture: the origin itself (host-checked)
+                    no = co;
+                } else {
+                    const double jx = -0.5 + 1.0 * unit31(w.next31());
+                    const double jy = -0.5 + 1.0 * unit31(w.next31());
+                    const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
+                    no = co + v3(dx, dy, 0);
+                }
+                X = dest - no;
+            } else {
+                // random_dir_no_norm (rtutility.h:189-203), then n + dir (main.c:163)
+                const double u = unit31(wa >> 1);
+                const double v = unit31(wb >> 1);
+                X = H.hn + normalize_unit(sampler_vec(u, v));
+                st.n += 2;
+            }
+            const V3 dn = normalize(X);
+            if (cam) {                                         // the new sample's primary ray
+                L.o = no;
+                L.d = dn;
+                if (AOM == AO_ON) L.cd = dn;
+                L.inc = v3(0, 0, 0);
+                L.rc = v3(1, 1, 1);
+                L.top_n2 = 1.0;
+                L.i = 0;
+                L.chain = true;
+                L.ao_cast = false;
+                L.state = SM_CAST;
+                st.start(pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1, rng);
+                st.n = 4;                                      // draws 0-3 were the camera's
+            } else {
+                L.finish_bounce(kp, dn, st, acc, H);
+            }
+        }
     }
-    Q.trace_out(kp, t_start, rounds);
+    if (kp.trace) {                  // diagnostics (RT_QUEUE_TRACE): per lane start, end, rounds, tasks
+        unsigned long long* q = kp.trace + ((size_t)blockIdx.x * 256 + threadIdx.x) * RT_TRACE_WORDS;
+        q[0] = (unsigned long long)t_start;
+        q[1] = (unsigned long long)wall_clock64();
+        q[2] = rounds;
+        q[3] = ntasks;
+    }
 }
 #endif
 
@@ -2909,44 +2705,31 @@ static void queue_occupancy(int& nb)
 {
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<SKY, AOM, QB>, 256, 0);
 }
-template <bool SKY, int AOM, int QB>
-static void queue_occupancy_c(int& nb)
-{
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_qc<SKY, AOM, QB>, 256, 0);
-}
 
 // Resident blocks of the queue kernel on this device (grid of render_kernel_q).
 // Cached per device and variant; rt_fill_canva may run on several host
 // threads at once (main.c's pthreads), so the cache is atomic (every thread
 // computes the same value).
 template <int QB>
-static void queue_occupancy_v(bool sky, bool ao, bool qc, int& nb)
+static void queue_occupancy_v(bool sky, bool ao, int& nb)
 {
-    if (qc && QB > 0) {
-        if (sky && ao) queue_occupancy_c<true, AO_ON, QB>(nb);
-        else if (sky) queue_occupancy_c<true, AO_OFF, QB>(nb);
-        else if (ao) queue_occupancy_c<false, AO_ON, QB>(nb);
-        else queue_occupancy_c<false, AO_OFF, QB>(nb);
-        return;
-    }
     if (sky && ao) queue_occupancy<true, AO_ON, QB>(nb);
     else if (sky) queue_occupancy<true, AO_OFF, QB>(nb);
     else if (ao) queue_occupancy<false, AO_ON, QB>(nb);
     else queue_occupancy<false, AO_OFF, QB>(nb);
 }
-static unsigned queue_grid(bool sky, bool ao, int qb, bool qc)
+static unsigned queue_grid(bool sky, bool ao, int qb)
 {
-    static std::atomic<int> cached[24][64];
+    static std::atomic<int> cached[12][64];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::atomic<int>& slot =
-        cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? 1 : 2) + (qc ? 12 : 0)][dev & 63];
+    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? 1 : 2)][dev & 63];
     int c = slot.load(std::memory_order_relaxed);
     if (c <= 0) {
         int nb = 0, ncu = 0;
-        if (qb == 0) queue_occupancy_v<0>(sky, ao, qc, nb);
-        else if (qb == 3) queue_occupancy_v<3>(sky, ao, qc, nb);
-        else queue_occupancy_v<4>(sky, ao, qc, nb);
+        if (qb == 0) queue_occupancy_v<0>(sky, ao, nb);
+        else if (qb == 3) queue_occupancy_v<3>(sky, ao, nb);
+        else queue_occupancy_v<4>(sky, ao, nb);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
         c = std::max(1, nb) * std::max(1, ncu);
         if (std::getenv("RT_QUEUE_VERBOSE")) std::fprintf(stderr, "render_kernel_q: %d blocks/CU x %d CUs -> %d\n", nb, ncu, c);
@@ -2959,15 +2742,8 @@ static unsigned queue_grid(bool sky, bool ao, int qb, bool qc)
 }
 
 template <int QB>
-static void queue_launch(bool sky, bool ao, bool qc, unsigned nb, hipStream_t st, const KParams& k2)
+static void queue_launch(bool sky, bool ao, unsigned nb, hipStream_t st, const KParams& k2)
 {
-    if (qc && QB > 0) {
-        if (sky && ao) hipLaunchKernelGGL((render_kernel_qc<true, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
-        else if (sky) hipLaunchKernelGGL((render_kernel_qc<true, AO_OFF, QB>), dim3(nb), dim3(256), 0, st, k2);
-        else if (ao) hipLaunchKernelGGL((render_kernel_qc<false, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
-        else hipLaunchKernelGGL((render_kernel_qc<false, AO_OFF, QB>), dim3(nb), dim3(256), 0, st, k2);
-        return;
-    }
     if (sky && ao) hipLaunchKernelGGL((render_kernel_q<true, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
     else if (sky) hipLaunchKernelGGL((render_kernel_q<true, AO_OFF, QB>), dim3(nb), dim3(256), 0, st, k2);
     else if (ao) hipLaunchKernelGGL((render_kernel_q<false, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
@@ -2989,11 +2765,7 @@ int launch_render(const KParams& kp, void* stream)
         // node visits per lane and round: 4 for shallow trees, 3 for deep ones
         // (kp.bvh_steps, host; compile-time per instantiation)
         const int qb = qbvh ? (kp.bvh_steps <= 3 ? 3 : 4) : 0;
-        // BVH scenes: closest hits compacted over the block (render_kernel_qc);
-        // RT_QC=0 selects render_kernel_q's per-lane walks (A/B)
-        static const bool qc_env = !(std::getenv("RT_QC") && std::atoi(std::getenv("RT_QC")) == 0);
-        const bool qc = qb > 0 && qc_env;
-        const unsigned nb = queue_grid(sky, ao, qb, qc);
+        const unsigned nb = queue_grid(sky, ao, qb);
         unsigned long long* tr = nullptr;
         const char* tf = std::getenv("RT_QUEUE_TRACE");
         if (tf) (void)hipMalloc((void**)&tr, (size_t)nb * 256 * RT_TRACE_WORDS * sizeof(unsigned long long));
@@ -3007,9 +2779,9 @@ int launch_render(const KParams& kp, void* stream)
         // chunk starts c*S/P in 32 bits when (P + 1) * S fits
         k2.qm_chunks = (unsigned long long)(kp.chunk_den + 1) * (unsigned long long)kp.S < (1ull << 32)
                            ? qdiv_magic(kp.chunk_den) : 0u;
-        if (qb == 3) queue_launch<3>(sky, ao, qc, nb, st, k2);
-        else if (qb == 4) queue_launch<4>(sky, ao, qc, nb, st, k2);
-        else queue_launch<0>(sky, ao, qc, nb, st, k2);
+        if (qb == 3) queue_launch<3>(sky, ao, nb, st, k2);
+        else if (qb == 4) queue_launch<4>(sky, ao, nb, st, k2);
+        else queue_launch<0>(sky, ao, nb, st, k2);
         if (tr) {
             std::vector<unsigned long long> h((size_t)nb * 256 * RT_TRACE_WORDS);
             (void)hipStreamSynchronize(st);
