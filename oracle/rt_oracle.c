@@ -13,6 +13,15 @@
  *
  * Compile with -ffp-contract=off: every + - * / is one IEEE rounding, in
  * the reference's association order.
+ *
+ * Pinning: the leaf functions (hit_sphere, hit_triangle, tri_uvmapping,
+ * camera, optics, pile, HSL, write_color_canva) against the reference's own
+ * headers compiled here (oracle/Makefile, tests/golden/kat_leaf.json); the
+ * composition of tracer / closest_hit / fill_canva against the reference's
+ * config-1 image md5 (sphere-only, no AO).  main.c itself
+ * cannot be built here (it includes <OpenImageDenoise/oidn.h>, absent), so
+ * the composition of the AO, refraction/IOR-stack, texture and alpha-hole
+ * branches is PARITY UNPINNED beyond those leaf KATs.
  */
 #define _GNU_SOURCE
 #include <math.h>

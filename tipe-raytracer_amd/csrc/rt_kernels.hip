@@ -64,6 +64,10 @@
 #endif
 static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x1p-20,
               "candidate half-width M must be >= 8 x the sqrt error bound 2^-47.2/sqrt(T1)");
+#ifndef RT_QTASK_TABLE              // sphere-scene queue kernel: tasks decoded per batch into LDS (A/B knob;
+                                    // RT_QUEUE must then be 64, one task per lane of a batch)
+#define RT_QTASK_TABLE 1
+#endif
 #ifndef RT_WAVES_PER_SIMD
 #define RT_WAVES_PER_SIMD 4
 #endif
@@ -75,6 +79,7 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #define RT_QUEUE 64                 // (tasks per atomic grab of a wave; 0: off)
 #endif
 static_assert(RT_QUEUE == 0 || RT_QUEUE >= 64, "a wave's grab (up to 64 lanes) must fit one batch");
+static_assert(!RT_QTASK_TABLE || RT_QUEUE == 64, "the task table holds one batch of 64 tasks per wave");
 #ifndef RT_WAVES_PER_SIMD_Q         // queue kernel occupancy bound
 #define RT_WAVES_PER_SIMD_Q RT_WAVES_PER_SIMD
 #endif
@@ -419,10 +424,14 @@ __device__ __forceinline__ unsigned short* bvh_stack()
 // The queue kernel's per-lane stack (BVH scenes): [kStackQ][256] uint16, 12 KiB,
 // which keeps the kernel at 4 blocks (16 waves) per CU; trees that could need
 // more entries (3 * depth4 + 1 > kStackQ) render with the fixed-grid kernel.
-constexpr int kStackQ = 24;
+// The QB = 4 instantiation serves shallow trees only (depth4 <= 4: at most 13
+// entries) and keeps 14, so its top-node cache and the task table fit the
+// same 40 KiB.
+constexpr int kStackQ = 24, kStackQ4 = 14;
+template <int QB>
 __device__ __forceinline__ unsigned short* bvh_stack_q()
 {
-    __shared__ unsigned short stkq_lds[kStackQ * 256];
+    __shared__ unsigned short stkq_lds[(QB == 4 ? kStackQ4 : kStackQ) * 256];
     return stkq_lds + threadIdx.x;
 }
 // ... and the block's copy of the tree's top nodes (RT_QB_TOP x 128 B; the
@@ -2262,6 +2271,32 @@ struct QPath {
     }
 };
 
+// Task t of a queue launch as render_kernel_q's LDS table entry: e[0] its
+// chunk-partial index chunk * band_rows * W + p (~0: past the last task),
+// e[1] the pixel g * W + x (~0: a padding row of the tiling, no work), e[2]
+// the row g, e[3], e[4] its first and end sample (rt.h rt_chunk_bound).
+constexpr int kTaskWords = 5;
+__device__ __forceinline__ void decode_task(KParamsK K, unsigned t, uint32_t e[kTaskWords])
+{
+    for (int j = 0; j < kTaskWords; ++j) e[j] = 0xffffffffu;
+    if (t >= K->npx_here * (unsigned)K->chunks) return;
+    unsigned p;
+    const unsigned chunk = udiv_q(t, K->npx_here, K->qm_npx, p);
+    e[0] = chunk * ((unsigned)K->band_rows * (unsigned)K->W) + p;
+    unsigned xr;
+    const unsigned row = udiv_q(p, (unsigned)K->W, K->qm_w, xr);
+    const int ly = K->band_y0 + (int)row;
+    if (ly >= K->local_rows) return;
+    unsigned yy;
+    const int lt = (int)udiv_q((unsigned)ly, (unsigned)K->tile_rows, K->qm_tile, yy);
+    const int g = K->row_base + (K->tile_first + lt * K->tile_step) * K->tile_rows + (int)yy;
+    if (g >= K->row_end) return;
+    e[1] = (uint32_t)g * (uint32_t)K->W + xr;
+    e[2] = (uint32_t)g;
+    e[3] = (uint32_t)chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk);
+    e[4] = (uint32_t)chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk + 1u);
+}
+
 template <bool SKY, int AOM, int QB>
 __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
 {
@@ -2282,6 +2317,12 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     int node = 0, sp = 0, win_orig = 0;      // BVH walk in flight (state SM_TRAV)
     unsigned chunk = 0, p = 0, pixel = 0;
     bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
+    // sphere / brute-force scenes (QB 0): each wave decodes its batches of tasks into LDS
+    // (not for QB 3, the deep-tree instantiation: there the table's registers
+    // cost spills, C4 -0.6 %; C2 +3.5 %, C3 +1.0 %, sweep +2.3 %)
+    constexpr bool TTAB = RT_QTASK_TABLE && QB != 3;
+    __shared__ uint32_t ttab_lds[TTAB ? 4 * kTaskWords * 64 : 1];
+    unsigned qidx = 0;               // (TTAB) partial index of the lane's task
     Stream st;                       // draw stream of the sample in flight (next31 for refraction / AO)
     st.start(0u, 0u, kp.key0, kp.key1, rng);
     // shallow trees (QB 4: depth4 <= 4, e.g. the 50-node sweep tree) keep
@@ -2316,7 +2357,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
             if (__ballot(L.state == SM_TRAV) != 0ull) {
                 const V3 dd = L.cast_dir();
                 const Ray32 r32 = ray32(L.o, dd, kp.bvh_rbox);
-                unsigned short* stk = bvh_stack_q();
+                unsigned short* stk = bvh_stack_q<QB>();
                 const BvhNode4* top = NTOP > 0 ? bvh_top_q() : nullptr;
 #pragma unroll 1
                 for (int j = 0; j < QB; ++j) {
@@ -2351,6 +2392,59 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
             unsigned t = 0;
             const unsigned nn = (unsigned)__popcll(nm), avail = qe - qb;
             const unsigned rank = (unsigned)__popcll(nm & ((1ull << lane) - 1ull));
+            if constexpr (TTAB) {
+                // a batch's 64 tasks are decoded once, by the whole wave, into the
+                // wave's LDS table when the batch is grabbed; a lane taking a task
+                // reads its entry: lanes taking the rest of the current batch
+                // before the new batch overwrites the table, the others after
+                uint32_t* tw = ttab_lds + (threadIdx.x >> 6) * (kTaskWords * 64);
+                const bool old = rank < avail;
+                uint32_t e[kTaskWords];
+                if (need && old) {
+                    const unsigned slot = (qb - (qe - RT_QUEUE)) + rank;
+#pragma unroll
+                    for (int j = 0; j < kTaskWords; ++j) e[j] = tw[j * 64 + slot];
+                }
+                if (avail < nn) {
+                    unsigned nb = 0;
+                    if (lane == __ffsll((long long)nm) - 1) nb = atomicAdd(K->task_ctr, (unsigned)RT_QUEUE);
+                    nb = __shfl(nb, __ffsll((long long)nm) - 1, 64);
+                    uint32_t d[kTaskWords];
+                    decode_task(K, nb + (unsigned)lane, d);
+#pragma unroll
+                    for (int j = 0; j < kTaskWords; ++j) tw[j * 64 + lane] = d[j];
+                    if (need && !old) {
+#pragma unroll
+                        for (int j = 0; j < kTaskWords; ++j) e[j] = tw[j * 64 + (rank - avail)];
+                    }
+                    qb = nb + (nn - avail);
+                    qe = nb + RT_QUEUE;
+                } else {
+                    qb += nn;
+                }
+                if (need) {
+                    ++ntasks;
+                    if (owns) {      // task done: its sums to the chunk partials
+                        double* q = K->partial + (size_t)qidx * 9;
+#pragma unroll
+                        for (int j = 0; j < 9; ++j) q[j] = acc[j * 256];
+                        owns = false;
+                    }
+                    if (e[0] == 0xffffffffu) {
+                        L.state = SM_DONE;
+                    } else if (e[1] != 0xffffffffu) {  // otherwise the lane takes its next task next round
+                        qidx = e[0];
+                        pixel = e[1];
+                        g = (int)e[2];
+                        x = (int)(pixel - e[2] * (unsigned)K->W);
+                        L.s = (int)e[3];
+                        s1 = (int)e[4];
+#pragma unroll
+                        for (int j = 0; j < 9; ++j) acc[j * 256] = 0.0;
+                        owns = true;
+                    }
+                }
+            } else {
             if (avail < nn) {        // a new batch (nn <= 64 <= RT_QUEUE): old tasks first
                 unsigned nb = 0;
                 if (lane == __ffsll((long long)nm) - 1) nb = atomicAdd(K->task_ctr, (unsigned)RT_QUEUE);
@@ -2395,6 +2489,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                         owns = true;
                     }
                 }
+            }
             }
         }
         if (__ballot(L.state != SM_DONE) == 0ull) break;     // every lane of the wave is done
@@ -2764,7 +2859,7 @@ int launch_render(const KParams& kp, void* stream)
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
         // node visits per lane and round: 4 for shallow trees, 3 for deep ones
         // (kp.bvh_steps, host; compile-time per instantiation)
-        const int qb = qbvh ? (kp.bvh_steps <= 3 ? 3 : 4) : 0;
+        const int qb = qbvh ? (kp.bvh_steps <= 3 || kp.bvh_stack > kStackQ4 ? 3 : 4) : 0;
         const unsigned nb = queue_grid(sky, ao, qb);
         unsigned long long* tr = nullptr;
         const char* tf = std::getenv("RT_QUEUE_TRACE");
