@@ -64,6 +64,9 @@
 #endif
 static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x1p-20,
               "candidate half-width M must be >= 8 x the sqrt error bound 2^-47.2/sqrt(T1)");
+#ifndef RT_AO_FIRST                 // AO scenes: the AO direction before the bounce direction (ROLE_AO)
+#define RT_AO_FIRST 1
+#endif
 #ifndef RT_QTASK_TABLE              // sphere-scene queue kernel: tasks decoded per batch into LDS (A/B knob;
                                     // RT_QUEUE must then be 64, one task per lane of a batch)
 #define RT_QTASK_TABLE 1
@@ -2061,7 +2064,19 @@ __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIM
 // to tracer; work whose result cannot reach the output is skipped: the
 // direction after the last bounce, and the AO cast of the last bounce
 // (tracer multiplies rayColor by it and then returns incomingLight).
-enum : int { ROLE_NONE = 0, ROLE_BOUNCE = 1, ROLE_CAMERA = 2 };
+enum : int { ROLE_NONE = 0, ROLE_BOUNCE = 1, ROLE_CAMERA = 2, ROLE_AO = 3, ROLE_PBOUNCE = 4 };
+// AO scenes (AOM == AO_ON), an opaque bounce whose draws start a Philox block
+// (draw n = 4k: the camera takes draws 0-3 and a shaded bounce with its AO
+// ray 4 more, so every such bounce in scenes without translucent surfaces or
+// alpha holes): the lane makes ONE direction per round.  ROLE_AO makes the AO
+// direction from draws n+2, n+3 right after the shading (ambient_occlusion,
+// main.c:96-103), keeping draws n, n+1 of the same block in the LDS cache;
+// after the AO cast, ROLE_PBOUNCE makes the bounce direction from them
+// (main.c:161-166) and the lerp.  The draws, and so the results, are the
+// reference's; each round's shared next-ray step then serves every lane that
+// needs a direction, instead of a second sampling pass for the AO ray in
+// finish_bounce, and the bounce direction is skipped when the AO factor
+// ends the path.
 
 // What resolve_hit leaves for next_ray / finish_bounce in the same round (not
 // live across rounds, so not in QPath: the cast and the BVH walk do not carry
@@ -2078,6 +2093,9 @@ struct QPath {
     double top_n2, best;
     int i, kind, win, s, state;
     bool chain, ao_cast;
+    bool pend;                       // (AO_ON) the bounce direction waits for the AO cast (ROLE_PBOUNCE)
+    V3 phn;                          // ... the bounce hit's normal
+    double prs;                      // ... and its reflectionStrength
 
     __device__ __forceinline__ V3 cast_dir() const { return AOM == AO_ON ? cd : d; }
 
@@ -2100,7 +2118,7 @@ struct QPath {
 
     // After a cast (state SM_RESOLVE).  Returns the role for next_ray, or
     // ROLE_NONE; a lane whose path is over gets state SM_CAM (sum added).
-    __device__ __forceinline__ int resolve_hit(const KParams& kp, double* acc, QHit& H)
+    __device__ __forceinline__ int resolve_hit(const KParams& kp, double* acc, QHit& H, uint32_t sn)
     {
         bool ended = false, add_inc = true;
         int role = ROLE_NONE;
@@ -2122,9 +2140,17 @@ struct QPath {
             ++i;                                         // the bounce after the AO cast
             ended = zero_rc(kp) || i >= kp.B;
             if (!ended) {
-                cd = d;
-                state = SM_CAST;
+                if (pend) {                              // its direction is still to be made
+                    role = ROLE_PBOUNCE;
+                    H.hn = phn;
+                    H.rs = prs;
+                    H.refr = H.hole = false;
+                } else {
+                    cd = d;
+                    state = SM_CAST;
+                }
             }
+            pend = false;
         } else if (kind == HIT_NONE) {                   // miss: the path ends, main.c:236-238
             if (chain) {
                 acc_add(acc, ACC_ALB, v3(0, 0, 0));
@@ -2179,8 +2205,16 @@ struct QPath {
                         role = ROLE_BOUNCE;
                     } else {
                         shade(kp, mat);
-                        if (zero_rc(kp) || i + 1 >= kp.B) ended = true;   // nothing more reaches the sum
-                        else role = ROLE_BOUNCE;
+                        if (zero_rc(kp) || i + 1 >= kp.B) {
+                            ended = true;                // nothing more reaches the sum
+                        } else if (AOM == AO_ON && RT_AO_FIRST && (sn & 3u) == 0u) {
+                            role = ROLE_AO;              // AO direction first (ROLE_AO above)
+                            pend = true;
+                            phn = H.hn;
+                            prs = mat.rs;
+                        } else {
+                            role = ROLE_BOUNCE;
+                        }
                     }
                 }
             }
@@ -2312,6 +2346,9 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     L.best = 0.0;
     L.i = 0; L.kind = HIT_NONE; L.win = -1; L.s = 0;
     L.chain = true; L.ao_cast = false;
+    L.pend = false;
+    L.phn = v3(0, 0, 0);
+    L.prs = 0.0;
     L.state = SM_CAM;                // s = 0 >= s1 = 0: takes a task first
     int x = 0, g = 0, s1 = 0;
     int node = 0, sp = 0, win_orig = 0;      // BVH walk in flight (state SM_TRAV)
@@ -2381,7 +2418,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
         H.hn = v3(0, 0, 0);
         H.rs = 0.0;
         H.refr = H.hole = false;
-        if (L.state == SM_RESOLVE) role = L.resolve_hit(kp, acc, H);
+        if (L.state == SM_RESOLVE) role = L.resolve_hit(kp, acc, H, st.n);
         // ---- 3. lanes whose task is done take the next one -----------------
         const bool need = L.state == SM_CAM && L.s >= s1;
         const unsigned long long nm = __ballot(need);
@@ -2505,27 +2542,41 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
         // ---- 4. next ray: bounce direction or camera ray (shared work) ----
         if (role != ROLE_NONE) {
             const bool cam = role == ROLE_CAMERA;
+            const bool aor = AOM == AO_ON && role == ROLE_AO, pbr = AOM == AO_ON && role == ROLE_PBOUNCE;
             // draws: a bounce uses draws n, n+1 of its sample (rtutility.h:
-            // 189-203); a camera ray draws 0-3 of sample s (main.c:265-269)
+            // 189-203); a camera ray draws 0-3 of sample s (main.c:265-269);
+            // ROLE_AO draws n+2, n+3 of block n/4 and keeps n, n+1 in the
+            // cache's words 0-1 for ROLE_PBOUNCE
             const uint32_t nd = cam ? 0u : st.n;
             const uint32_t sa = nd & 3u, sb = (nd + 1u) & 3u;
             uint32_t wa = 0, wb = 0;
-            if (!cam && sa != 0u) wa = rng[sa * 256];          // cached word of the current block
-            if (!cam && sb != 0u && sa != 0u) wb = rng[sb * 256];
             Philox blk{0, 0, 0, 0};
-            if (cam || sa == 0u || sb == 0u) {                 // a new block: one Philox for both roles
-                const uint32_t bi = cam ? 0u : ((nd + (sa == 0u ? 0u : 1u)) >> 2);
-                blk = philox4x32_10(bi, 0u, pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1);
-                if (!cam) {                                     // keep the rest of the block
-                    rng[256] = blk.w1;
-                    rng[512] = blk.w2;
-                    rng[768] = blk.w3;
+            if (pbr) {
+                wa = rng[0];
+                wb = rng[256];
+            } else {
+                if (!cam && !aor && sa != 0u) wa = rng[sa * 256];          // cached word of the current block
+                if (!cam && !aor && sb != 0u && sa != 0u) wb = rng[sb * 256];
+                if (cam || aor || sa == 0u || sb == 0u) {                 // a new block: one Philox for every role
+                    const uint32_t bi = cam ? 0u : ((nd + (sa == 0u ? 0u : 1u)) >> 2);
+                    blk = philox4x32_10(bi, 0u, pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1);
+                    if (aor) {                                      // the bounce's draws, for ROLE_PBOUNCE
+                        rng[0] = blk.w0;
+                        rng[256] = blk.w1;
+                    } else if (!cam) {                              // keep the rest of the block
+                        rng[256] = blk.w1;
+                        rng[512] = blk.w2;
+                        rng[768] = blk.w3;
+                    }
                 }
-            }
-            if (!cam) {
-                if (sa == 0u) wa = blk.w0;
-                if (sb == 0u) wb = blk.w0;
-                else if (sa == 0u) wb = blk.w1;
+                if (aor) {
+                    wa = blk.w2;
+                    wb = blk.w3;
+                } else if (!cam) {
+                    if (sa == 0u) wa = blk.w0;
+                    if (sb == 0u) wb = blk.w0;
+                    else if (sa == 0u) wb = blk.w1;
+                }
             }
             V3 X;
             V3 no = v3(0, 0, 0);
@@ -2559,7 +2610,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 const double u = unit31(wa >> 1);
                 const double v = unit31(wb >> 1);
                 X = H.hn + normalize_unit(sampler_vec(u, v));
-                st.n += 2;
+                st.n += aor ? 0u : pbr ? 4u : 2u;
             }
             const V3 dn = normalize(X);
             if (cam) {                                         // the new sample's primary ray
@@ -2575,6 +2626,15 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 L.state = SM_CAST;
                 st.start(pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1, rng);
                 st.n = 4;                                      // draws 0-3 were the camera's
+            } else if (aor) {                                  // ambient_occlusion's cast (main.c:96-103)
+                L.cd = dn;
+                L.ao_cast = true;
+                L.state = SM_CAST;
+            } else if (pbr) {                                  // main.c:161-166 after the AO cast
+                const V3 reflected_dir = L.d - muls(H.hn, 2 * dot(L.d, H.hn));
+                L.d = dn + muls(reflected_dir - dn, H.rs);
+                L.cd = L.d;
+                L.state = SM_CAST;
             } else {
                 L.finish_bounce(kp, dn, st, acc, H);
             }
