@@ -2094,7 +2094,7 @@ struct QPath {
     int i, kind, win, s, state;
     bool chain, ao_cast;
     bool pend;                       // (AO_ON) the bounce direction waits for the AO cast (ROLE_PBOUNCE)
-    V3 phn;                          // ... the bounce hit's normal
+    int pkw;                         // ... the bounce hit: win | kind << 30 (its normal is recomputed at o)
     double prs;                      // ... and its reflectionStrength
 
     __device__ __forceinline__ V3 cast_dir() const { return AOM == AO_ON ? cd : d; }
@@ -2142,7 +2142,14 @@ struct QPath {
             if (!ended) {
                 if (pend) {                              // its direction is still to be made
                     role = ROLE_PBOUNCE;
-                    H.hn = phn;
+                    const int pw = pkw & 0x3fffffff;     // the bounce hit's normal (o is its hit point)
+                    if ((pkw >> 30) == HIT_SPHERE) {
+                        const SphGeo sg = kp.sph[pw];
+                        H.hn = normalize(o - v3(sg.cx, sg.cy, sg.cz));
+                    } else {
+                        const TriGeo tg = kp.tri[pw];
+                        H.hn = normalize(v3(tg.nx, tg.ny, tg.nz));
+                    }
                     H.rs = prs;
                     H.refr = H.hole = false;
                 } else {
@@ -2210,7 +2217,7 @@ struct QPath {
                         } else if (AOM == AO_ON && RT_AO_FIRST && (sn & 3u) == 0u) {
                             role = ROLE_AO;              // AO direction first (ROLE_AO above)
                             pend = true;
-                            phn = H.hn;
+                            pkw = win | (kind << 30);
                             prs = mat.rs;
                         } else {
                             role = ROLE_BOUNCE;
@@ -2347,7 +2354,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     L.i = 0; L.kind = HIT_NONE; L.win = -1; L.s = 0;
     L.chain = true; L.ao_cast = false;
     L.pend = false;
-    L.phn = v3(0, 0, 0);
+    L.pkw = 0;
     L.prs = 0.0;
     L.state = SM_CAM;                // s = 0 >= s1 = 0: takes a task first
     int x = 0, g = 0, s1 = 0;
