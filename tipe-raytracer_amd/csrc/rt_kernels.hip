@@ -2123,29 +2123,18 @@ struct QPath {
         bool ended = false, add_inc = true;
         int role = ROLE_NONE;
         if (AOM == AO_ON && ao_cast) {
-            // ambient_occlusion's tail, main.c:104-115.  sqrt and the two
-            // divisions run the exact cores (rt_device_math.h) on lanes inside
-            // their guards: |df|^2 in [2^-760, 2^760] (distance then within
-            // [2^-380, 2^380]), best in [2^-400, 2^400], AO in [2^-400, 2^400]
-            // and occ = +0 or within [2^-900, 2^900]; other lanes the IEEE ops
+            // ambient_occlusion's tail, main.c:104-115
             const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
             double occ = 0.0;
             if (kind != HIT_NONE) {
                 const V3 hp = o + muls(cast_dir(), best);
                 const V3 df = hp - o;
-                const double x2 = dot(df, df);
-                double att;
-                if (x2 >= 0x1p-760 && x2 <= 0x1p760 && best >= 0x1p-400 && best <= 0x1p400)
-                    att = div_core(sqrt_core(x2), best, rcp_refined(best));
-                else
-                    att = sqrt(x2) / best;
+                const double distance = sqrt(dot(df, df));
+                double att = distance / best;
                 att = pm_pow(att, AO);
                 occ = occ + att;
             }
-            occ = occ / 1.0;
-            const double aocc = fabs(occ);
-            occ = (AO >= 0x1p-400 && AO <= 0x1p400 && (occ == 0.0 || (aocc >= 0x1p-900 && aocc <= 0x1p900)))
-                      ? div_core(occ, AO, rcp_refined(AO)) : occ / AO;
+            occ = (occ / 1.0) / AO;
             rc = mulv(rc, v3(occ, occ, occ));
             ao_cast = false;
             ++i;                                         // the bounce after the AO cast
