@@ -10,6 +10,7 @@ B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras"
 timeout -k 10 900 python -u -m pytest tests/ -x -v -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 &&
 timeout -k 10 200 python3 -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
 timeout -k 10 300 python3 bench.py > $OUT/bench.json 2> $OUT/bench.err &&
+ps -u "$(id -u)" -o pid,ppid,etimes,args > $OUT/ps_after_bench.txt &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-extras > $OUT/kt.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt_cfg -o run --output-format csv -- python3 tools/bench_configs.py > $OUT/kt_cfg.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- $B > $OUT/fetch.log 2>&1 &&
