@@ -95,6 +95,29 @@ def test_device_math_bitexact():
     assert (tipe_rt.selftest_math(6, fs.astype(np.float64), n) == np.sqrt(fs).astype(np.float64)).all()
 
 
+def test_device_pow_special_and_wide_inputs():
+    """pm_pow's device form (one straight-line log/exp with the special cases
+    selected afterwards, rt_device_math.h) against oracle/pm_math.h's branchy
+    pm_pow: zeros, negatives, infinities, NaN, subnormals, exp's overflow and
+    underflow limits, and wide random x, for the AO intensities a scene can
+    set (fractional, integer, negative, huge, infinite, NaN)."""
+    o = oracle_ffi.oracle()
+    rng = np.random.default_rng(23)
+    inf, nan = np.inf, np.nan
+    xs_edge = [0.0, -0.0, -1.0, -2.5, inf, -inf, nan, 5e-324, 1e-310, 2.0 ** -1022, 2.0 ** -1022 * (1 - 2.0 ** -52),
+               1.0, 1 + 2.0 ** -52, 1 - 2.0 ** -53, 0.5, 2.0, 1e300, 1e-300, 1.7976931348623157e308]
+    ys_edge = [2.5, -2.5, 0.5, 0.1, 3.0, -3.0, 100.5, -100.5, 1e10, -1e10, inf, -inf, nan, 0.0, 64.0, 65.0, 1e-300]
+    n = 4096
+    xr = np.concatenate([rng.uniform(0, 4, n), 10.0 ** rng.uniform(-320, 308, n), 1 + rng.uniform(-1e-12, 1e-12, n)])
+    yr = rng.choice([2.5, 0.7, -1.3, 7.25, 300.5], len(xr))
+    x = np.concatenate([np.repeat(xs_edge, len(ys_edge)), xr])
+    y = np.concatenate([np.tile(ys_edge, len(xs_edge)), yr])
+    got = tipe_rt.selftest_math(3, np.stack([x, y], 1).ravel(), len(x))
+    want = np.array([o.oracle_pm_pow(a, b) for a, b in zip(x, y)])
+    same = (got.view(np.uint64) == want.view(np.uint64)) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), list(zip(x[~same], y[~same], got[~same], want[~same]))[:6]
+
+
 def test_device_normalize_fast_path_is_ieee():
     """normalize() skips the sqrt/division range fixups on in-range lanes and
     shares 1/|a| (rt_kernels.hip); it must equal a / sqrt(a.a) in IEEE f64

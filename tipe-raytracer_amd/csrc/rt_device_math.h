@@ -432,6 +432,17 @@ __device__ __forceinline__ double pm_atan2(double y, double x)
 // ---- pow ---------------------------------------------------------------------
 __device__ __forceinline__ double pm_from_bits(unsigned long long b) { return __longlong_as_double((long long)b); }
 
+// The log/exp kernels run once per AO cast (ambient_occlusion's pow,
+// main.c:111).  Their coefficients are read one scalar load each from its own
+// opaque base (KCV1): a Horner chain reading 11-12 of them from one base got
+// its loads merged into s_load_dwordx16, whose 16 SGPRs the AO kernels then
+// spilled to VGPR lanes and read back one by one (32 v_writelane/v_readlane
+// per pow in the C4 kernel).
+#define KCV1(i) (kcb()[(i)])
+
+// pm_log for every x the pow path feeds it (special x give finite values that
+// pm_pow discards): m in (0.70, 1.42], so 2 + f is in [1.7, 2.5] and f = m - 1
+// is 0 or of magnitude >= 2^-53; the quotient is div_core0's exact IEEE one.
 __device__ __forceinline__ double pm_log(cdptr b, double x)
 {
     const unsigned long long u = (unsigned long long)__double_as_longlong(x);
@@ -439,33 +450,44 @@ __device__ __forceinline__ double pm_log(cdptr b, double x)
     double m = pm_from_bits((u & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
     if (m > KCV(b, KC_SQRT2)) { m = m * 0.5; e = e + 1; }
     const double f = m - 1.0;
-    const double s = f / (2.0 + f);
+    const double d = 2.0 + f;
+    const double s = div_core0(f, d, rcp_refined(d));
     const double z = s * s;
-    const double t = KCV(b, KC_L1) + z * (KCV(b, KC_L2) + z * (KCV(b, KC_L3) + z * (KCV(b, KC_L4) +
-                     z * (KCV(b, KC_L5) + z * (KCV(b, KC_L6) + z * (KCV(b, KC_L7) + z * (KCV(b, KC_L8) +
-                     z * (KCV(b, KC_L9) + z * (KCV(b, KC_L10) + z * KCV(b, KC_L11))))))))));
+    const double t = KCV1(KC_L1) + z * (KCV1(KC_L2) + z * (KCV1(KC_L3) + z * (KCV1(KC_L4) +
+                     z * (KCV1(KC_L5) + z * (KCV1(KC_L6) + z * (KCV1(KC_L7) + z * (KCV1(KC_L8) +
+                     z * (KCV1(KC_L9) + z * (KCV1(KC_L10) + z * KCV1(KC_L11))))))))));
     const double lm = 2.0 * s + (2.0 * s) * (z * t);
     const double ed = (double)e;
-    return ed * KCV(b, KC_LN2_HI) + (lm + ed * KCV(b, KC_LN2_LO));
+    return ed * KCV1(KC_LN2_HI) + (lm + ed * KCV1(KC_LN2_LO));
 }
 
+// pm_exp without branches: the kernel runs on t clamped to [-708, 709] (the
+// same t wherever it is used) and the out-of-range and NaN results are
+// selected afterwards, as pm_math.h's early returns give them.
 __device__ __forceinline__ double pm_exp(cdptr b, double t)
 {
-    if (t > 709.0) return __longlong_as_double(0x7ff0000000000000ll);
-    if (t < -708.0) return 0.0;
-    const double kd = rint(t * KCV(b, KC_INV_LN2));
-    const double r = (t - kd * KCV(b, KC_LN2_HI)) - kd * KCV(b, KC_LN2_LO);
-    const double p = 1.0 + r * (1.0 + r * (KCV(b, KC_E2) + r * (KCV(b, KC_E3) + r * (KCV(b, KC_E4) +
-                     r * (KCV(b, KC_E5) + r * (KCV(b, KC_E6) + r * (KCV(b, KC_E7) + r * (KCV(b, KC_E8) +
-                     r * (KCV(b, KC_E9) + r * (KCV(b, KC_E10) + r * (KCV(b, KC_E11) + r * (KCV(b, KC_E12) +
-                     r * KCV(b, KC_E13)))))))))))));
+    const double tc = fmin(fmax(t, -708.0), 709.0);
+    const double kd = rint(tc * KCV1(KC_INV_LN2));
+    const double r = (tc - kd * KCV1(KC_LN2_HI)) - kd * KCV1(KC_LN2_LO);
+    const double p = 1.0 + r * (1.0 + r * (KCV1(KC_E2) + r * (KCV1(KC_E3) + r * (KCV1(KC_E4) +
+                     r * (KCV1(KC_E5) + r * (KCV1(KC_E6) + r * (KCV1(KC_E7) + r * (KCV1(KC_E8) +
+                     r * (KCV1(KC_E9) + r * (KCV1(KC_E10) + r * (KCV1(KC_E11) + r * (KCV1(KC_E12) +
+                     r * KCV1(KC_E13)))))))))))));
     const int k = (int)kd;
     const int k1 = k / 2, k2 = k - k1;
     const double s1 = pm_from_bits((unsigned long long)(k1 + 1023) << 52);
     const double s2 = pm_from_bits((unsigned long long)(k2 + 1023) << 52);
-    return (p * s1) * s2;
+    double res = (p * s1) * s2;
+    res = t > 709.0 ? __longlong_as_double(0x7ff0000000000000ll) : res;
+    res = t < -708.0 ? 0.0 : res;
+    return t != t ? t + t : res;               // NaN t: pm_math.h's arithmetic propagates it
 }
 
+// pm_pow (oracle/pm_math.h): a wave-uniform y (the AO intensity) keeps the
+// first two cases uniform branches; the per-lane cases of x are selects over
+// one log/exp evaluation (the subnormal scaling folded into its argument), so
+// the AO kernels run one straight-line copy instead of five nested divergent
+// branches around two inlined copies of log.
 __device__ __forceinline__ double pm_pow(double x, double y)
 {
     if (y == 0.0) return 1.0;
@@ -482,12 +504,13 @@ __device__ __forceinline__ double pm_pow(double x, double y)
     }
     const cdptr b = kcb();
     const double inf = __longlong_as_double(0x7ff0000000000000ll);
-    if (x != x || y != y) return x + y;
-    if (x == 0.0) return y > 0.0 ? 0.0 : inf;
-    if (x < 0.0) return (x - x) / (x - x);
-    if (x == inf) return y > 0.0 ? inf : 0.0;
-    if (x < 0x1p-1022) return pm_exp(b, y * (pm_log(b, x * 0x1p54) - 54.0 * KCV(b, KC_LN2)));
-    return pm_exp(b, y * pm_log(b, x));
+    const bool sub = x < 0x1p-1022;
+    const double l = pm_log(b, sub ? x * 0x1p54 : x);
+    double res = pm_exp(b, y * (sub ? l - 54.0 * KCV1(KC_LN2) : l));
+    res = x == inf ? (y > 0.0 ? inf : 0.0) : res;
+    res = x < 0.0 ? (x - x) / (x - x) : res;
+    res = x == 0.0 ? (y > 0.0 ? 0.0 : inf) : res;
+    return (x != x || y != y) ? x + y : res;
 }
 
 }  // namespace rt
