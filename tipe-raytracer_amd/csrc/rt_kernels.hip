@@ -492,22 +492,49 @@ __device__ __forceinline__ float cull32(const KParams& kp, double best)
 // The four child boxes of a node: hit flags and near distances.  The entry
 // and exit planes of each axis are picked by the sign of inv (one 16-byte
 // row of lo or hi per axis: BvhNode4 stores lo[3][4] then hi[3][4]).
+// Node rows of the HBM tree at 32-bit byte offsets from the tree's
+// wave-uniform base: the loads take the scalar-base + 32-bit vector-offset
+// form, one v_add_u32 per row instead of 64-bit address arithmetic.
+__device__ __forceinline__ float4 bvh_row(const KParams& kp, uint32_t off)
+{
+    return *(const float4*)((const char*)kp.bvh + off);
+}
+// nd: the node (an LDS or generic pointer); or, with nd == nullptr, the HBM
+// node at byte offset nb (C4 +2.3 %, sweep +1.2 % over 64-bit addresses)
 __device__ __forceinline__ void box4(const KParams& kp, const BvhNode4* nd, const Ray32& r, float cull, bool h[4],
-                                     float tn[4])
+                                     float tn[4], int Ch[4], int Cn[4], uint32_t nb = 0)
 {
     const float nsabs = (float)(-kp.bvh_sabs) * (1.0f + 0x1p-22f);
     const float4* rows = (const float4*)nd;             // rows 0-2: lo x/y/z, rows 3-5: hi x/y/z
     const int sx = (int)(__float_as_uint(r.ix) >> 31) * 3, sy = (int)(__float_as_uint(r.iy) >> 31) * 3,
               sz = (int)(__float_as_uint(r.iz) >> 31) * 3;
-    const float4 px = rows[sx], py = rows[1 + sy], pz = rows[2 + sz];
-    const float4 qx = rows[3 - sx], qy = rows[4 - sy], qz = rows[5 - sz];
+    float4 px, py, pz, qx, qy, qz;
+    int4 cnt4;
+    if (nd == nullptr) {
+        px = bvh_row(kp, nb + (uint32_t)(sx * 16));
+        py = bvh_row(kp, nb + (uint32_t)((1 + sy) * 16));
+        pz = bvh_row(kp, nb + (uint32_t)((2 + sz) * 16));
+        qx = bvh_row(kp, nb + (uint32_t)((3 - sx) * 16));
+        qy = bvh_row(kp, nb + (uint32_t)((4 - sy) * 16));
+        qz = bvh_row(kp, nb + (uint32_t)((5 - sz) * 16));
+        const float4 c4 = bvh_row(kp, nb + (uint32_t)offsetof(BvhNode4, count));
+        const float4 h4 = bvh_row(kp, nb + (uint32_t)offsetof(BvhNode4, child));
+        cnt4 = make_int4(__float_as_int(c4.x), __float_as_int(c4.y), __float_as_int(c4.z), __float_as_int(c4.w));
+        Ch[0] = __float_as_int(h4.x); Ch[1] = __float_as_int(h4.y); Ch[2] = __float_as_int(h4.z); Ch[3] = __float_as_int(h4.w);
+    } else {
+        px = rows[sx]; py = rows[1 + sy]; pz = rows[2 + sz];
+        qx = rows[3 - sx]; qy = rows[4 - sy]; qz = rows[5 - sz];
+        cnt4 = make_int4(nd->count[0], nd->count[1], nd->count[2], nd->count[3]);
+        for (int c = 0; c < 4; ++c) Ch[c] = nd->child[c];
+    }
+    Cn[0] = cnt4.x; Cn[1] = cnt4.y; Cn[2] = cnt4.z; Cn[3] = cnt4.w;
     const float Px[4] = {px.x, px.y, px.z, px.w}, Py[4] = {py.x, py.y, py.z, py.w}, Pz[4] = {pz.x, pz.y, pz.z, pz.w};
     const float Qx[4] = {qx.x, qx.y, qx.z, qx.w}, Qy[4] = {qy.x, qy.y, qy.z, qy.w}, Qz[4] = {qz.x, qz.y, qz.z, qz.w};
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         const float tmin = fmaxf(fmaxf(fmaf(Px[c], r.ix, r.ax), fmaf(Py[c], r.iy, r.ay)), fmaf(Pz[c], r.iz, r.az));
         const float tmax = fminf(fminf(fmaf(Qx[c], r.ix, r.bx), fmaf(Qy[c], r.iy, r.by)), fmaf(Qz[c], r.iz, r.bz));
-        h[c] = nd->count[c] >= 0 && tmin <= tmax && tmax >= nsabs && tmin <= cull;
+        h[c] = Cn[c] >= 0 && tmin <= tmax && tmax >= nsabs && tmin <= cull;
         tn[c] = tmin;
     }
 }
@@ -523,21 +550,22 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
 {
     // NTOP > 0: the first NTOP nodes (breadth-first: the top levels) are read
     // from the block's LDS copy `top`, the rest from HBM/L2
-    const BvhNode4* nd = (NTOP > 0 && node < NTOP) ? top + node : kp.bvh + node;
+    const BvhNode4* nd = (NTOP > 0 && node < NTOP) ? top + node : nullptr;
     if (COUNT) {
         cnt.c[RT_CNT_BVH_NODES] += 1;
         wave_slots(cnt, RT_CNT_BVH_LANE_SLOTS);
     }
     bool h[4];
     float tn[4];
-    box4(kp, nd, r32, cull32(kp, best), h, tn);
+    int Ch[4], Cn[4];
+    box4(kp, nd, r32, cull32(kp, best), h, tn, Ch, Cn, (uint32_t)node * (uint32_t)sizeof(BvhNode4));
     int next = -1;
     float tnext = 0.0f;
     unsigned lm = 0;                                     // hit leaf slots
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         if (!h[c]) continue;
-        const int ch = nd->child[c], n = nd->count[c];
+        const int ch = Ch[c], n = Cn[c];
         if (n > 0) {
             lm |= 1u << c;
         } else if (next < 0) {
@@ -563,8 +591,8 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
         if (k >= kend) {
             const int c = __ffs(lm) - 1;
             lm &= lm - 1u;
-            k = nd->child[c];
-            kend = k + nd->count[c];
+            k = c == 0 ? Ch[0] : c == 1 ? Ch[1] : c == 2 ? Ch[2] : Ch[3];
+            kend = k + (c == 0 ? Cn[0] : c == 1 ? Cn[1] : c == 2 ? Cn[2] : Cn[3]);
             if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)(kend - k);
         }
         tri_test<COUNT, CU>(kp, k, o, d, best, kind, win, win_orig);
@@ -1330,7 +1358,8 @@ __device__ __forceinline__ bool coop_step(const KParams& kp, const V3 o, const V
     }
     bool h[4];
     float tn[4];
-    box4(kp, nd, r32, cull32(kp, best), h, tn);
+    int Ch[4], Cn[4];
+    box4(kp, nd, r32, cull32(kp, best), h, tn, Ch, Cn);
     int next = -1;
     float tnext = 0.0f;
     unsigned lm = 0;
@@ -1731,7 +1760,8 @@ __device__ __forceinline__ int closest_f32(const KParams& kp, const F32Scene& fs
             const BvhNode4* nd = kp.bvh + node;
             bool h[4];
             float tn[4];
-            box4(kp, nd, r32, cull32(kp, (double)best), h, tn);
+            int Ch[4], Cn[4];
+            box4(kp, nd, r32, cull32(kp, (double)best), h, tn, Ch, Cn);
             int next = -1;
             float tnext = 0.0f;
 #pragma unroll
