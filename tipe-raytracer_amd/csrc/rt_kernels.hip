@@ -377,12 +377,14 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
 // the caller's order (BVH leaf order), an equal dst replaces a triangle
 // winner with a larger caller index (orig).  det >= 1e-6 >= 2^-400 puts
 // 1/det on the exact fast division (div_core).
-template <bool COUNT, bool CU = false>
+// O32 (BVH leaves: a tree holds < 65535 nodes, so k * sizeof(TriGeo) < 2^32):
+// the records are read at 32-bit byte offsets from the array's scalar base.
+template <bool COUNT, bool CU = false, bool O32 = false>
 __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, const V3 d, double& best, int& kind,
                                          int& win, int& win_orig)
 {
     const double eps = CU ? 0.00001 : 0.0000001;     // triangle.hu:262 / mesh.h:88
-    const TriGeo g = kp.tri[k];
+    const TriGeo g = O32 ? *(const TriGeo*)((const char*)kp.tri + (uint32_t)k * (uint32_t)sizeof(TriGeo)) : kp.tri[k];
     const double det = -(d.x * g.nx + d.y * g.ny + d.z * g.nz);
     if (det >= 1E-6) {
         const V3 ao = v3(o.x - g.ax, o.y - g.ay, o.z - g.az);
@@ -392,7 +394,8 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
         else invDet = 1 / det;
         const double dst = (ao.x * g.nx + ao.y * g.ny + ao.z * g.nz) * invDet;
         if (dst >= eps && dst <= best) {
-            const int orig = kp.tri_orig ? kp.tri_orig[k] : k;
+            const int orig = !kp.tri_orig ? k
+                             : O32 ? *(const int*)((const char*)kp.tri_orig + (uint32_t)k * 4u) : kp.tri_orig[k];
             if (dst < best || (kind == HIT_TRI && orig < win_orig)) {
                 const double u = (g.acx * dao.x + g.acy * dao.y + g.acz * dao.z) * invDet;
                 const double v = -(g.abx * dao.x + g.aby * dao.y + g.abz * dao.z) * invDet;
@@ -595,7 +598,7 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
             kend = k + (c == 0 ? Cn[0] : c == 1 ? Cn[1] : c == 2 ? Cn[2] : Cn[3]);
             if (COUNT) cnt.c[RT_CNT_BVH_TRI_TESTS] += (unsigned long long)(kend - k);
         }
-        tri_test<COUNT, CU>(kp, k, o, d, best, kind, win, win_orig);
+        tri_test<COUNT, CU, true>(kp, k, o, d, best, kind, win, win_orig);
         ++k;
     }
     if (next >= 0) {
