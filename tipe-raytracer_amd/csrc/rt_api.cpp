@@ -141,6 +141,7 @@ struct rt_device_scene {
     TriTex* tri_tex = nullptr;
     DevMat* texels = nullptr;
     BvhNode4* bvh = nullptr;         // 4-wide BVH; null: no BVH (few triangles)
+    BvhNodeH* bvhh = nullptr;        // the same tree in 64-byte nodes, or null (does not fit binary16)
     DevMat* sky = nullptr;           // sky texels (scene->sky_mat_list), or null
     DevMat* tri_mat = nullptr;       // rt_triangle.mat per triangle (RT_SEM_CUDA)
     double cbb[6] = {0, 0, 0, 0, 0, 0};   // triangles' box (RT_SEM_CUDA hit_BBox)
@@ -230,6 +231,7 @@ void free_scene(rt_device_scene* s)
     (void)hipFree(s->tri_tex);
     (void)hipFree(s->texels);
     (void)hipFree(s->bvh);
+    (void)hipFree(s->bvhh);
     (void)hipFree(s->sky);
     (void)hipFree(s->tri_mat);
     (void)hipFree(s->sph_rinv);
@@ -343,6 +345,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
                    (!kp.useAO || (AO > 0.0 && AO <= 1000.0 && std::fmax(sc->coord_max, cam) <= 0x1p20));
     if (sc->bvh && p->accel == RT_ACCEL_AUTO && cam <= sc->r_scene) {
         kp.bvh = sc->bvh;
+        kp.bvhh = sc->bvhh;
         kp.bvh_srel = sc->s_rel;
         kp.bvh_sabs = sc->s_abs;
         kp.bvh_rbox = sc->bvh_rbox;
@@ -828,9 +831,17 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
                     for (int a = 0; a < 3; ++a) rb = std::max({rb, std::fabs(nd.lo[a][c]), std::fabs(nd.hi[a][c])});
         ds->bvh_rbox = std::isfinite(rb) ? rb * (1.0f + 0x1p-20f) : HUGE_VALF;
     }
+    std::vector<BvhNodeH> nodesh;
+    {
+        float rbh = 0.0f;
+        if (!bvh.nodes4.empty() && pack_bvh_h(bvh.nodes4, nodesh, rbh))
+            ds->bvh_rbox = std::max(ds->bvh_rbox, rbh * (1.0f + 0x1p-20f));   // one bound serves both forms
+        else
+            nodesh.clear();
+    }
     if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_cand, cand)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
         (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels)) ||
-        (rc = upload(&ds->bvh, bvh.nodes4)) || (rc = upload(&ds->tri_orig, bvh.order)) ||
+        (rc = upload(&ds->bvh, bvh.nodes4)) || (rc = upload(&ds->bvhh, nodesh)) || (rc = upload(&ds->tri_orig, bvh.order)) ||
         (rc = upload(&ds->sky, sky)) || (rc = upload(&ds->sph_rinv, sph_rinv)) || (rc = upload(&ds->sph_disp, sph_disp)) ||
         (rc = upload(&ds->tri_mat, tri_mat))) {
         free_scene(ds);

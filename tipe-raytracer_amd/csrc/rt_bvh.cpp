@@ -321,4 +321,113 @@ bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
     return true;
 }
 
+// ---- 64-byte nodes (BvhNodeH) ------------------------------------------------
+namespace {
+
+// binary16 <-> double by bits (normal, subnormal, zero; no inf/NaN here)
+double h2d(unsigned short h)
+{
+    const int e = (h >> 10) & 0x1f, m = h & 0x3ff;
+    const double v = e == 0 ? std::ldexp((double)m, -24) : std::ldexp((double)(m | 0x400), e - 25);
+    return (h & 0x8000) ? -v : v;
+}
+// the binary16 bit pattern next above / below h (finite h; false at overflow)
+bool h_up(unsigned short& h)
+{
+    if (h == 0x8000) h = 0x0001;                       // -0 -> smallest positive
+    else if (h & 0x8000) h = (unsigned short)(h - 1);  // negative: toward zero
+    else {
+        if (h >= 0x7bff) return false;                 // 65504 has no finite successor
+        h = (unsigned short)(h + 1);
+    }
+    return true;
+}
+bool h_down(unsigned short& h)
+{
+    if (h == 0x0000) h = 0x8001;
+    else if (h & 0x8000) {
+        if (h >= 0xfbff) return false;
+        h = (unsigned short)(h + 1);
+    } else h = (unsigned short)(h - 1);
+    return true;
+}
+// the largest binary16 <= x, or the smallest >= x (x finite); false beyond 65504
+bool h_round(double x, bool up, unsigned short& h)
+{
+    if (!(std::fabs(x) <= 65504.0)) return false;
+    // nearest by search from a coarse start: frexp/ldexp give the bits directly
+    const double ax = std::fabs(x);
+    unsigned short b;
+    if (ax < std::ldexp(1.0, -14)) {
+        b = (unsigned short)std::nearbyint(ax * std::ldexp(1.0, 24));
+    } else {
+        int e;
+        const double f = std::frexp(ax, &e);           // ax = f 2^e, f in [0.5, 1)
+        long m = std::lrint(std::ldexp(f, 11));        // 11 significant bits
+        if (m == 2048) { m = 1024; ++e; }
+        b = (unsigned short)(((e - 1 + 15) << 10) | (m & 0x3ff));
+        if (((b >> 10) & 0x1f) >= 31) return false;
+    }
+    h = (unsigned short)(x < 0.0 ? (b | 0x8000) : b);
+    if (x == 0.0) h = 0;
+    while (up ? h2d(h) < x : h2d(h) > x)
+        if (!(up ? h_up(h) : h_down(h))) return false;
+    return true;
+}
+
+}  // namespace
+
+bool pack_bvh_h(const std::vector<BvhNode4>& nodes4, std::vector<BvhNodeH>& out, float& rbox)
+{
+    out.assign(nodes4.size(), BvhNodeH{});
+    double rb = 0.0;
+    for (size_t i = 0; i < nodes4.size(); ++i) {
+        const BvhNode4& n = nodes4[i];
+        BvhNodeH& h = out[i];
+        double lo[3] = {HUGE_VAL, HUGE_VAL, HUGE_VAL};
+        for (int c = 0; c < 4; ++c)
+            if (n.count[c] >= 0)
+                for (int a = 0; a < 3; ++a) lo[a] = std::fmin(lo[a], (double)n.lo[a][c]);
+        double org[3];
+        for (int a = 0; a < 3; ++a) {
+            if (!std::isfinite(lo[a])) lo[a] = 0.0;
+            if (!h_round(lo[a], false, h.org[a])) return false;
+            org[a] = h2d(h.org[a]);
+            rb = std::fmax(rb, std::fabs(org[a]));
+        }
+        h.cnt = 0;
+        for (int c = 0; c < 4; ++c) {
+            int nib;
+            if (n.count[c] < 0) nib = 15;
+            else if (n.count[c] > 14) return false;
+            else nib = n.count[c];
+            if (n.count[c] >= 0 && (n.child[c] < 0 || n.child[c] > 0xffff)) return false;
+            h.cnt = (unsigned short)(h.cnt | (nib << (4 * c)));
+            h.child[c] = (unsigned short)(n.count[c] >= 0 ? n.child[c] : 0);
+            for (int a = 0; a < 3; ++a) {
+                if (n.count[c] < 0) {
+                    h.plo[a][c] = h.phi[a][c] = 0;
+                    continue;
+                }
+                // org + rel in double is exact (two binary16 values), so the
+                // comparisons below are exact; step outward until they hold
+                unsigned short ql, qh;
+                if (!h_round((double)n.lo[a][c] - org[a], false, ql) || !h_round((double)n.hi[a][c] - org[a], true, qh))
+                    return false;
+                while (org[a] + h2d(ql) > (double)n.lo[a][c])
+                    if (!h_down(ql)) return false;
+                while (org[a] + h2d(qh) < (double)n.hi[a][c])
+                    if (!h_up(qh)) return false;
+                h.plo[a][c] = ql;
+                h.phi[a][c] = qh;
+                rb = std::fmax(rb, std::fmax(std::fabs(org[a] + h2d(ql)), std::fabs(org[a] + h2d(qh))));
+                rb = std::fmax(rb, std::fabs(org[a]) + std::fmax(std::fabs(h2d(ql)), std::fabs(h2d(qh))));
+            }
+        }
+    }
+    rbox = (float)rb;
+    if ((double)rbox < rb) rbox = std::nextafter(rbox, HUGE_VALF);
+    return std::isfinite(rbox);
+}
+
 }  // namespace rt

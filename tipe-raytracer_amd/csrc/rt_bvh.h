@@ -35,6 +35,30 @@ static_assert(sizeof(BvhNode4) == 128, "BvhNode4");
 
 constexpr int kStack4 = 48;         // kernel LDS stack entries (3 pushes per 4-wide level)
 
+// The same 4-wide node in 64 bytes for the queue kernel (r03): binary16
+// planes relative to a binary16 node origin, rounded outward, so that
+//   org + plo <= the float lo bound and org + phi >= the float hi bound
+// hold exactly (the box only grows: every culling decision stays
+// conservative).  Rows as BvhNode4's: plo[a] (a = x, y, z), then phi[a], 8
+// bytes each (four children); the 16-byte tail holds the origin, the four
+// 4-bit counts (0 internal, 1-14 leaf of that many triangles, 15 empty) and
+// the 16-bit child indices (node, or first triangle in leaf order).  The
+// kernel's slab test reads the halves straight into v_fma_mix_f32.
+struct BvhNodeH {
+    unsigned short plo[3][4];
+    unsigned short phi[3][4];
+    unsigned short org[3];
+    unsigned short cnt;             // count of child c in bits 4c..4c+3
+    unsigned short child[4];
+};
+static_assert(sizeof(BvhNodeH) == 64, "BvhNodeH");
+
+// Packs nodes4 into BvhNodeH; false when a value does not fit (|coordinate|
+// beyond binary16's range, a leaf of more than 14 triangles, a child index
+// above 65535).  rbox: >= |org| + |plane| over every node (the slab
+// margin's coordinate bound for the packed planes).
+bool pack_bvh_h(const std::vector<BvhNode4>& nodes4, std::vector<BvhNodeH>& out, float& rbox);
+
 struct BvhBuild {
     std::vector<BvhNode> nodes;     // binary tree, node 0 = root split
     std::vector<BvhNode4> nodes4;   // collapsed 4-wide tree, node 0 = root

@@ -27,6 +27,7 @@
 namespace rt {
 
 struct BvhNode4;                                      // rt_bvh.h
+struct BvhNodeH;                                      // rt_bvh.h (64-byte form)
 
 struct SphGeo { double cx, cy, cz, r2; };            // r2 = radius*radius (sphere.h:22)
 // Candidate-pass record (rt_kernels.hip spheres_closest): center and
@@ -76,6 +77,7 @@ struct KParams {
     const DevMat* texels;
     const double* uni;       // U_COUNT doubles
     const BvhNode4* bvh;     // 4-wide triangle BVH (rt_bvh.h), or null: brute-force scan
+    const BvhNodeH* bvhh;    // the same tree in 64-byte nodes (the queue kernel's), or null
     const int* tri_orig;     // triangle k's index in the caller's list (null: k)
     const DevMat* sky;       // sky texels when sky mode is on, else null
     const DevMat* tri_mat;   // rt_triangle.mat per triangle (leaf order with a BVH): RT_SEM_CUDA

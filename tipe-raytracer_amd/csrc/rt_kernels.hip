@@ -440,14 +440,20 @@ __device__ __forceinline__ unsigned short* bvh_stack_q()
     __shared__ unsigned short stkq_lds[(QB == 4 ? kStackQ4 : kStackQ) * 256];
     return stkq_lds + threadIdx.x;
 }
-// ... and the block's copy of the tree's top nodes (RT_QB_TOP x 128 B; the
-// block then needs <= 40 KiB of LDS, still 4 blocks per CU)
+// ... and the block's copy of the tree's top nodes (RT_QB_TOP x 128 B, or
+// twice as many 64-byte nodes; the block then needs <= 40 KiB of LDS, still
+// 4 blocks per CU)
 #ifndef RT_QB_TOP
 #define RT_QB_TOP 40
 #endif
-__device__ __forceinline__ BvhNode4* bvh_top_q()
+// the queue kernel walks the 64-byte nodes (BvhNodeH) when the scene has them
+#ifndef RT_QNODE_H
+#define RT_QNODE_H 1
+#endif
+template <class NODE, int N>
+__device__ __forceinline__ NODE* bvh_top_q()
 {
-    __shared__ BvhNode4 top_lds[RT_QB_TOP > 0 ? RT_QB_TOP : 1];
+    __shared__ NODE top_lds[N > 0 ? N : 1];
     return top_lds;
 }
 // Conservative single-precision slab test (the culling only has to be a
@@ -542,18 +548,81 @@ __device__ __forceinline__ void box4(const KParams& kp, const BvhNode4* nd, cons
     }
 }
 
+// box4 on the 64-byte node (BvhNodeH, the queue kernel's): each plane is
+// org + rel with binary16 org and rel (rt_bvh.h), so the entry distance is
+// fma(rel, inv, A) with A = fma(org, inv, a) per axis and node, the halves
+// read straight into v_fma_mix_f32.  Against box4's single fma the extra
+// rounding of A adds at most u(|org| + |o|)|inv| + uE (u = 2^-24), and
+// with rbox >= |org| + |rel| (host) the total stays below E / 3.
+__device__ __forceinline__ float h16lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu)); }
+__device__ __forceinline__ float h16hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
+__device__ __forceinline__ void box4h(const KParams& kp, const BvhNodeH* nd, uint32_t nb, const Ray32& r, float cull,
+                                      bool h[4], float tn[4], int Ch[4], int Cn[4])
+{
+    const float nsabs = (float)(-kp.bvh_sabs) * (1.0f + 0x1p-22f);
+    const uint32_t sx = (__float_as_uint(r.ix) >> 31) * 3u, sy = (__float_as_uint(r.iy) >> 31) * 3u,
+                   sz = (__float_as_uint(r.iz) >> 31) * 3u;
+    uint2 px, py, pz, qx, qy, qz;
+    uint4 t;
+#ifndef RT_HNODE_WHOLE
+#define RT_HNODE_WHOLE 1
+#endif
+    if (RT_HNODE_WHOLE && nd == nullptr) {               // HBM: the whole node in four 16-byte loads,
+        const uint4* q = (const uint4*)((const char*)kp.bvhh + nb);   // rows selected by sign
+        const uint4 r0 = q[0], r1 = q[1], r2 = q[2];
+        t = q[3];
+        const uint2 lx = make_uint2(r0.x, r0.y), ly = make_uint2(r0.z, r0.w), lz = make_uint2(r1.x, r1.y);
+        const uint2 hx = make_uint2(r1.z, r1.w), hy = make_uint2(r2.x, r2.y), hz = make_uint2(r2.z, r2.w);
+        px = sx ? hx : lx; qx = sx ? lx : hx;
+        py = sy ? hy : ly; qy = sy ? ly : hy;
+        pz = sz ? hz : lz; qz = sz ? lz : hz;
+    } else if (nd == nullptr) {                          // HBM: 32-bit offsets from the scalar base
+        const char* b = (const char*)kp.bvhh;
+        px = *(const uint2*)(b + (nb + sx * 8u));
+        py = *(const uint2*)(b + (nb + (1u + sy) * 8u));
+        pz = *(const uint2*)(b + (nb + (2u + sz) * 8u));
+        qx = *(const uint2*)(b + (nb + (3u - sx) * 8u));
+        qy = *(const uint2*)(b + (nb + (4u - sy) * 8u));
+        qz = *(const uint2*)(b + (nb + (5u - sz) * 8u));
+        t = *(const uint4*)(b + (nb + 48u));
+    } else {                                             // the block's LDS copy of the top nodes
+        const uint2* rows = (const uint2*)nd;
+        px = rows[sx]; py = rows[1u + sy]; pz = rows[2u + sz];
+        qx = rows[3u - sx]; qy = rows[4u - sy]; qz = rows[5u - sz];
+        t = *(const uint4*)((const char*)nd + 48);
+    }
+    const float Ax = fmaf(h16lo(t.x), r.ix, r.ax), Ay = fmaf(h16hi(t.x), r.iy, r.ay), Az = fmaf(h16lo(t.y), r.iz, r.az);
+    const float Bx = fmaf(h16lo(t.x), r.ix, r.bx), By = fmaf(h16hi(t.x), r.iy, r.by), Bz = fmaf(h16lo(t.y), r.iz, r.bz);
+    const uint32_t cn = t.y >> 16;
+    Ch[0] = (int)(t.z & 0xffffu); Ch[1] = (int)(t.z >> 16); Ch[2] = (int)(t.w & 0xffffu); Ch[3] = (int)(t.w >> 16);
+    const float Px[4] = {h16lo(px.x), h16hi(px.x), h16lo(px.y), h16hi(px.y)};
+    const float Py[4] = {h16lo(py.x), h16hi(py.x), h16lo(py.y), h16hi(py.y)};
+    const float Pz[4] = {h16lo(pz.x), h16hi(pz.x), h16lo(pz.y), h16hi(pz.y)};
+    const float Qx[4] = {h16lo(qx.x), h16hi(qx.x), h16lo(qx.y), h16hi(qx.y)};
+    const float Qy[4] = {h16lo(qy.x), h16hi(qy.x), h16lo(qy.y), h16hi(qy.y)};
+    const float Qz[4] = {h16lo(qz.x), h16hi(qz.x), h16lo(qz.y), h16hi(qz.y)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int nib = (int)((cn >> (4 * c)) & 15u);
+        Cn[c] = nib == 15 ? -1 : nib;
+        const float tmin = fmaxf(fmaxf(fmaf(Px[c], r.ix, Ax), fmaf(Py[c], r.iy, Ay)), fmaf(Pz[c], r.iz, Az));
+        const float tmax = fminf(fminf(fmaf(Qx[c], r.ix, Bx), fmaf(Qy[c], r.iy, By)), fmaf(Qz[c], r.iz, Bz));
+        h[c] = nib != 15 && tmin <= tmax && tmax >= nsabs && tmin <= cull;
+        tn[c] = tmin;
+    }
+}
+
 // One node visit: the four child boxes, the triangles of the hit leaves, then
 // the next node (nearest hit internal child, else the stack top).  Returns
 // false when the traversal is over.  tris_bvh loops it to the end; the
 // resumable trace (render_sm) runs a bounded number of visits per round.
-template <bool COUNT, bool CU, int NTOP = 0>
+template <bool COUNT, bool CU, int NTOP = 0, bool H = false>
 __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3 d, const Ray32& r32,
                                          unsigned short* stk, int& node, int& sp, double& best, int& kind,
-                                         int& win, int& win_orig, Cnt& cnt, const BvhNode4* top = nullptr)
+                                         int& win, int& win_orig, Cnt& cnt, const void* top = nullptr)
 {
     // NTOP > 0: the first NTOP nodes (breadth-first: the top levels) are read
-    // from the block's LDS copy `top`, the rest from HBM/L2
-    const BvhNode4* nd = (NTOP > 0 && node < NTOP) ? top + node : nullptr;
+    // from the block's LDS copy `top`, the rest from HBM/L2; H: 64-byte nodes
     if (COUNT) {
         cnt.c[RT_CNT_BVH_NODES] += 1;
         wave_slots(cnt, RT_CNT_BVH_LANE_SLOTS);
@@ -561,7 +630,13 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
     bool h[4];
     float tn[4];
     int Ch[4], Cn[4];
-    box4(kp, nd, r32, cull32(kp, best), h, tn, Ch, Cn, (uint32_t)node * (uint32_t)sizeof(BvhNode4));
+    const bool in_top = NTOP > 0 && node < NTOP;
+    if (H)
+        box4h(kp, in_top ? (const BvhNodeH*)top + node : nullptr, (uint32_t)node * (uint32_t)sizeof(BvhNodeH), r32,
+              cull32(kp, best), h, tn, Ch, Cn);
+    else
+        box4(kp, in_top ? (const BvhNode4*)top + node : nullptr, r32, cull32(kp, best), h, tn, Ch, Cn,
+             (uint32_t)node * (uint32_t)sizeof(BvhNode4));
     int next = -1;
     float tnext = 0.0f;
     unsigned lm = 0;                                     // hit leaf slots
@@ -2404,11 +2479,13 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     st.start(0u, 0u, kp.key0, kp.key1, rng);
     // shallow trees (QB 4: depth4 <= 4, e.g. the 50-node sweep tree) keep
     // their top nodes in LDS: sweep +5.7 %; deep ones gain nothing (C4 -0.5 %)
-    constexpr int NTOP = QB == 4 ? RT_QB_TOP : 0;
+    constexpr bool HN = RT_QNODE_H != 0 && QB == 3;     // deep trees walk 64-byte nodes (host: kp.bvhh set)
+    using QNode = std::conditional_t<HN, BvhNodeH, BvhNode4>;
+    constexpr int NTOP = QB == 4 ? RT_QB_TOP * (int)(sizeof(BvhNode4) / sizeof(QNode)) : 0;
     if (NTOP > 0) {                          // the tree's top nodes into LDS, once per block
-        float4* dst = (float4*)bvh_top_q();
-        const float4* src = (const float4*)kp.bvh;
-        const int n = min(NTOP, kp.bvh_nodes) * (int)(sizeof(BvhNode4) / sizeof(float4));
+        float4* dst = (float4*)bvh_top_q<QNode, NTOP>();
+        const float4* src = HN ? (const float4*)kp.bvhh : (const float4*)kp.bvh;
+        const int n = min(NTOP, kp.bvh_nodes) * (int)(sizeof(QNode) / sizeof(float4));
         for (int i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
         __syncthreads();
     }
@@ -2435,12 +2512,12 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 const V3 dd = L.cast_dir();
                 const Ray32 r32 = ray32(L.o, dd, kp.bvh_rbox);
                 unsigned short* stk = bvh_stack_q<QB>();
-                const BvhNode4* top = NTOP > 0 ? bvh_top_q() : nullptr;
+                const QNode* top = NTOP > 0 ? bvh_top_q<QNode, NTOP>() : nullptr;
 #pragma unroll 1
                 for (int j = 0; j < QB; ++j) {
                     if (L.state == SM_TRAV) {
                         Cnt cnt;
-                        if (!bvh_step<false, false, NTOP>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind, L.win,
+                        if (!bvh_step<false, false, NTOP, HN>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind, L.win,
                                                            win_orig, cnt, top))
                             L.state = SM_RESOLVE;
                     }
@@ -2952,7 +3029,9 @@ static unsigned qdiv_magic(unsigned d) { return d ? (unsigned)(0xffffffffull / d
 int launch_render(const KParams& kp, void* stream)
 {
 #if RT_QUEUE > 0
-    const bool qbvh = kp.bvh != nullptr && kp.bvh_stack <= kStackQ;
+    // (the deep-tree instantiation walks kp.bvhh: a tree without the 64-byte
+    // form renders with the fixed-grid kernel)
+    const bool qbvh = kp.bvh != nullptr && kp.bvh_stack <= kStackQ && (!RT_QNODE_H || kp.bvhh != nullptr);
     if (kp.task_ctr && kp.chunks > 1 && (!kp.bvh || qbvh) && !kp.cuda && !kp.f32 && !kp.sums) {
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
