@@ -384,7 +384,17 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
                                          int& win, int& win_orig)
 {
     const double eps = CU ? 0.00001 : 0.0000001;     // triangle.hu:262 / mesh.h:88
-    const TriGeo g = O32 ? *(const TriGeo*)((const char*)kp.tri + (uint32_t)k * (uint32_t)sizeof(TriGeo)) : kp.tri[k];
+    TriGeo g;
+    if (O32) {
+        // the whole record in six 16-byte loads and ONE wait: left to itself
+        // the compiler sinks the A/AB/AC loads below the det test, a second
+        // dependent round trip per leaf test
+        g = *(const TriGeo*)((const char*)kp.tri + (uint32_t)k * (uint32_t)sizeof(TriGeo));
+        asm volatile("" : "+v"(g.ax), "+v"(g.ay), "+v"(g.az), "+v"(g.abx), "+v"(g.aby), "+v"(g.abz), "+v"(g.acx),
+                     "+v"(g.acy), "+v"(g.acz), "+v"(g.nx), "+v"(g.ny), "+v"(g.nz));
+    } else {
+        g = O32 ? *(const TriGeo*)((const char*)kp.tri + (uint32_t)k * (uint32_t)sizeof(TriGeo)) : kp.tri[k];
+    }
     const double det = -(d.x * g.nx + d.y * g.ny + d.z * g.nz);
     if (det >= 1E-6) {
         const V3 ao = v3(o.x - g.ax, o.y - g.ay, o.z - g.az);
@@ -564,11 +574,9 @@ __device__ __forceinline__ void box4h(const KParams& kp, const BvhNodeH* nd, uin
                    sz = (__float_as_uint(r.iz) >> 31) * 3u;
     uint2 px, py, pz, qx, qy, qz;
     uint4 t;
-#ifndef RT_HNODE_WHOLE
-#define RT_HNODE_WHOLE 1
-#endif
-    if (RT_HNODE_WHOLE && nd == nullptr) {               // HBM: the whole node in four 16-byte loads,
-        const uint4* q = (const uint4*)((const char*)kp.bvhh + nb);   // rows selected by sign
+    {                                                    // the whole node in four 16-byte loads (HBM at
+        const uint4* q = nd ? (const uint4*)nd                         // 32-bit offsets, or the LDS copy),
+                            : (const uint4*)((const char*)kp.bvhh + nb);   // rows selected by sign
         const uint4 r0 = q[0], r1 = q[1], r2 = q[2];
         t = q[3];
         const uint2 lx = make_uint2(r0.x, r0.y), ly = make_uint2(r0.z, r0.w), lz = make_uint2(r1.x, r1.y);
@@ -576,20 +584,6 @@ __device__ __forceinline__ void box4h(const KParams& kp, const BvhNodeH* nd, uin
         px = sx ? hx : lx; qx = sx ? lx : hx;
         py = sy ? hy : ly; qy = sy ? ly : hy;
         pz = sz ? hz : lz; qz = sz ? lz : hz;
-    } else if (nd == nullptr) {                          // HBM: 32-bit offsets from the scalar base
-        const char* b = (const char*)kp.bvhh;
-        px = *(const uint2*)(b + (nb + sx * 8u));
-        py = *(const uint2*)(b + (nb + (1u + sy) * 8u));
-        pz = *(const uint2*)(b + (nb + (2u + sz) * 8u));
-        qx = *(const uint2*)(b + (nb + (3u - sx) * 8u));
-        qy = *(const uint2*)(b + (nb + (4u - sy) * 8u));
-        qz = *(const uint2*)(b + (nb + (5u - sz) * 8u));
-        t = *(const uint4*)(b + (nb + 48u));
-    } else {                                             // the block's LDS copy of the top nodes
-        const uint2* rows = (const uint2*)nd;
-        px = rows[sx]; py = rows[1u + sy]; pz = rows[2u + sz];
-        qx = rows[3u - sx]; qy = rows[4u - sy]; qz = rows[5u - sz];
-        t = *(const uint4*)((const char*)nd + 48);
     }
     const float Ax = fmaf(h16lo(t.x), r.ix, r.ax), Ay = fmaf(h16hi(t.x), r.iy, r.ay), Az = fmaf(h16lo(t.y), r.iz, r.az);
     const float Bx = fmaf(h16lo(t.x), r.ix, r.bx), By = fmaf(h16hi(t.x), r.iy, r.by), Bz = fmaf(h16lo(t.y), r.iz, r.bz);
@@ -2479,7 +2473,9 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     st.start(0u, 0u, kp.key0, kp.key1, rng);
     // shallow trees (QB 4: depth4 <= 4, e.g. the 50-node sweep tree) keep
     // their top nodes in LDS: sweep +5.7 %; deep ones gain nothing (C4 -0.5 %)
-    constexpr bool HN = RT_QNODE_H != 0 && QB == 3;     // deep trees walk 64-byte nodes (host: kp.bvhh set)
+    // deep trees (QB 3) walk the 64-byte nodes (host: kp.bvhh set); the shallow
+    // ones keep their LDS copy in 128-byte nodes (64-byte: sweep -0.8 %)
+    constexpr bool HN = RT_QNODE_H != 0 && QB == 3;
     using QNode = std::conditional_t<HN, BvhNodeH, BvhNode4>;
     constexpr int NTOP = QB == 4 ? RT_QB_TOP * (int)(sizeof(BvhNode4) / sizeof(QNode)) : 0;
     if (NTOP > 0) {                          // the tree's top nodes into LDS, once per block
