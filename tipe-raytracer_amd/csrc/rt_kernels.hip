@@ -379,13 +379,22 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
 // 1/det on the exact fast division (div_core).
 // O32 (BVH leaves: a tree holds < 65535 nodes, so k * sizeof(TriGeo) < 2^32):
 // the records are read at 32-bit byte offsets from the array's scalar base.
-template <bool COUNT, bool CU = false, bool O32 = false>
+// UNI (the brute-force scan, k wave-uniform): the record through the scalar
+// unit (s_load into SGPRs, read by the VALU as scalar operands), no vector
+// memory instructions per triangle.
+template <bool COUNT, bool CU = false, bool O32 = false, bool UNI = false>
 __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, const V3 d, double& best, int& kind,
                                          int& win, int& win_orig)
 {
     const double eps = CU ? 0.00001 : 0.0000001;     // triangle.hu:262 / mesh.h:88
     TriGeo g;
-    if (O32) {
+    if (UNI) {
+        const cdptr t = (cdptr)kp.tri + 12 * k;
+        g.ax = t[0]; g.ay = t[1]; g.az = t[2];
+        g.abx = t[3]; g.aby = t[4]; g.abz = t[5];
+        g.acx = t[6]; g.acy = t[7]; g.acz = t[8];
+        g.nx = t[9]; g.ny = t[10]; g.nz = t[11];
+    } else if (O32) {
         // the whole record in six 16-byte loads and ONE wait: left to itself
         // the compiler sinks the A/AB/AC loads below the det test, a second
         // dependent round trip per leaf test
@@ -738,7 +747,7 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
     } else if (BVH) {
         tris_bvh<COUNT, CU>(kp, o, d, best, kind, win, win_orig, cnt);
     } else {
-        for (int k = 0; k < kp.nt; ++k) tri_test<COUNT, CU>(kp, k, o, d, best, kind, win, win_orig);
+        for (int k = 0; k < kp.nt; ++k) tri_test<COUNT, CU, false, true>(kp, k, o, d, best, kind, win, win_orig);
     }
     t_best = best;
     idx = win;
