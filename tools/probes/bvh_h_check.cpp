@@ -30,7 +30,10 @@ int main()
     if (!build_bvh(tri.data(), (int)tri.size(), r, b)) { std::printf("no bvh\n"); return 1; }
     std::vector<BvhNodeH> h;
     float rbox = 0;
-    if (!pack_bvh_h(b.nodes4, h, rbox)) { std::printf("pack failed\n"); return 1; }
+    if (!pack_bvh_h(b.nodes4, h, rbox)) {      // does not fit binary16: the kernel keeps 128-byte nodes
+        std::printf("{\"nodes\": %zu, \"packed\": false}\n", b.nodes4.size());
+        return 0;
+    }
     long bad = 0;
     double grow = 0.0, vol = 0.0;
     for (size_t i = 0; i < h.size(); ++i)
@@ -49,7 +52,7 @@ int main()
             }
             grow += g; vol += e;
         }
-    std::printf("{\"nodes\": %zu, \"depth4\": %d, \"violations\": %ld, \"volume_growth\": %.6f, \"rbox\": %.6g}\n",
+    std::printf("{\"nodes\": %zu, \"packed\": true, \"depth4\": %d, \"violations\": %ld, \"volume_growth\": %.6f, \"rbox\": %.6g}\n",
                 h.size(), b.depth4, bad, grow / vol, rbox);
     return bad != 0;
 }
