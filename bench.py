@@ -5,14 +5,20 @@
 
 One step = one full frame of config C2 (README 10-sphere Cornell box,
 1200x900, 1000 spp, 6 bounces; Philox stream, seed 1010) rendered into HBM.
-With N > 1 (launched one rank per GPU by torch.distributed.run) the frame is
+With N > 1 the bench runs one rank per GPU: either launched by
+torch.distributed.run (RANK/WORLD_SIZE set), or, when `--gpus N` is given
+without that environment, this script starts the N rank processes itself
+(spawn_ranks: the parent never initialises the GPU, and fails with exit 2
+if fewer than N GPUs are visible).  The frame is
 split into cyclic 1-row tiles (row t -> rank t mod N), each rank renders its
 tiles, the tiles' colour (the canva plane: write_color_canva integers, exact
 in float32, so 12 B/px -- SURVEY §8(e)'s float3 colour payload; `--gather
 all` sends canva + albedo + normal as doubles, 72 B/px, for a denoiser) is
 gathered to rank 0 over RCCL (torch.distributed.gather, backend "nccl") and
 rank 0 un-permutes it (rt_assemble_async): total work per step is fixed, so
-scaling is "strong".
+scaling is "strong".  At N > 1 rank 0 also times `single_process`: the
+library's own one-process multi-device frame (rt_render_gather_async over
+the N devices, peer copies over xGMI), the path a C caller of rt.h uses.
 
 Rank 0 prints ONE JSON line.  Besides the C2 headline it carries (N = 1,
 rank 0): `configs` (C3, C4, C5 and the 10-sphere/100-triangle sweep scene at
@@ -361,6 +367,101 @@ def end_to_end(scene, spheres, cam, reps=2):
     return out
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args, argv):
+    """`python bench.py --gpus N` with no torch.distributed environment: start
+    N rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as
+    torch.distributed.run sets them, rendezvous on 127.0.0.1) and return the
+    exit code.  This parent never touches the GPU (torch.cuda.device_count()
+    does not initialise it on ROCm), so no GPU process is ever replaced by
+    exec; the ranks are children.  With the nccl (RCCL) backend every rank
+    needs its own device: fewer than N visible devices is an error (exit 2),
+    never a silent N = 1 run.  Rank 0 prints the JSON line."""
+    import signal
+    import subprocess
+    n = args.gpus
+    visible = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and visible < n:
+        print("bench.py: --gpus %d needs %d visible GPUs, found %d" % (n, n, visible), file=sys.stderr)
+        return 2
+    if visible < 1:
+        print("bench.py: no GPU visible", file=sys.stderr)
+        return 2
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+    old = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print("bench.py: rank %d exited with %d; stopping the others" % (procs.index(p), c),
+                          file=sys.stderr)
+                    stop()
+            time.sleep(0.2)
+    finally:
+        stop()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except Exception:
+                p.kill()
+        signal.signal(signal.SIGTERM, old)
+    return rc
+
+
+def single_process_leg(scene, p, world, devs, steps, verify_ref=None):
+    """§8(e)'s in-library path for a C caller: one process, rt_init over the N
+    devices, rt_render_gather_async per frame (every device renders its cyclic
+    1-row tiles on a pooled stream, the canva planes travel to the first
+    device by peer copies over xGMI and are assembled there).  Timed over
+    `steps` frames after one warm-up frame; canva only, as the bench's gather."""
+    L = tipe_rt.lib()
+    tipe_rt.check(L.rt_init(len(devs), (C.c_int * len(devs))(*devs)))
+    dev = torch.device("cuda", devs[0])
+    st = torch.cuda.current_stream(dev)
+    try:
+        full = torch.empty((H, W, 3), dtype=torch.float64, device=dev)
+        tipe_rt.render_gather_async(scene, p, TILE_ROWS, full.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        ok = None if verify_ref is None else bool(torch.equal(full, verify_ref))
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            tipe_rt.render_gather_async(scene, p, TILE_ROWS, full.data_ptr(), stream=st.cuda_stream)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+    finally:
+        L.rt_shutdown()
+        tipe_rt.check(L.rt_init(0, None))
+    rec = {"value": round(W * H * SPP * steps / dt / 1e6, 3), "unit": "Msamples/s", "devices": list(devs),
+           "distinct_devices": len(set(devs)), "steps": steps, "ms_per_step": round(dt / steps * 1e3, 3),
+           "entry_point": "rt_render_gather_async (include/rt/rt.h)", "payload": "canva plane, float64"}
+    if ok is not None:
+        rec["verified_vs_single_device"] = ok
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -382,9 +483,21 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: gather through host copies (rehearsing N>1 with all ranks on one GPU); "
                          "nccl (= RCCL) is the measured configuration")
+    ap.add_argument("--no-single-process", action="store_true",
+                    help="N>1: skip the single_process leg (rt_render_gather_async over the N devices)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args, sys.argv[1:]))
+    if torch.cuda.device_count() < 1:
+        print("bench.py: no GPU visible", file=sys.stderr)
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE %d; rendering on the %d ranks launched" % (args.gpus, world, world),
+              file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     gpu = local_rank if args.dist_backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
@@ -476,6 +589,7 @@ def main():
         elapsed = float(t.item())
 
     verified = None
+    ref = None
     if args.verify and world > 1 and rank == 0:
         ref = torch.empty((3, H, W, 3), dtype=torch.float64, device=dev)
         tipe_rt.render_async(ds, p, tipe_rt.band_tiling(0, H - 1), ref[0].data_ptr(), ref[1].data_ptr(),
@@ -485,6 +599,23 @@ def main():
         verified = all(bool(torch.equal(ref[:npl], f)) for f in used)
         if not verified:
             print("verify: assembled frame differs from the single-device frame", file=sys.stderr)
+
+    # --- the library's own single-process multi-device frame (N > 1) --------
+    single = None
+    if world > 1 and not args.no_single_process:
+        # host-side barriers (gloo), so the other ranks wait without a
+        # collective kernel spinning on the devices rank 0 now renders on
+        cpu_group = dist.new_group(backend="gloo")
+        dist.barrier(group=cpu_group)
+        if rank == 0:
+            ndev = torch.cuda.device_count()
+            devs = [r if args.dist_backend == "nccl" else r % max(1, ndev) for r in range(world)]
+            single = single_process_leg(scene, p, world, devs, max(1, min(args.steps, 5)),
+                                        None if ref is None else ref[0])
+            if single.get("verified_vs_single_device") is False:
+                print("verify: rt_render_gather_async frame differs from the single-device frame", file=sys.stderr)
+        dist.barrier(group=cpu_group)
+        torch.cuda.set_device(dev)
 
     # --- kernel-only timing with HIP events on the launch stream ------------
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -570,6 +701,11 @@ def main():
         }
         if verified is not None:
             rec["verified_vs_single_device"] = verified
+        if world > 1:
+            rec["config"]["devices"] = len({r if args.dist_backend == "nccl" else r % max(1, torch.cuda.device_count())
+                                            for r in range(world)})
+        if single is not None:
+            rec["single_process"] = single
         if world == 1 and not args.no_extras:
             rec["configs"] = configs_extra(dev, stream, cam)
             rec["end_to_end"] = end_to_end(scene, spheres, cam)

@@ -184,6 +184,12 @@ void rt_params_init(rt_params* p);
 int  rt_init(int ndev, const int* devices);
 void rt_shutdown(void);
 const char* rt_last_error(void);
+/* Name of the render kernel the calling thread's last render launch used
+ * ("render_kernel_q<QB=0|3|4>" = the task-queue kernel without a BVH / with
+ * a deep / shallow tree, "render_kernel<BVH>" / "render_kernel" = the
+ * fixed-grid kernels, "render_kernel_cuda", "render_kernel_f32"); "none"
+ * before the first.  Diagnostics and tests. */
+const char* rt_last_render_kernel(void);
 const char* rt_version(void);
 int  rt_device_count(void);
 
@@ -282,6 +288,16 @@ int rt_gather_async(int world, const int* src_devices, const rt_color* const* lo
                     int rows_per_rank, int W, int H, int dst_device, rt_color* out, void* hip_stream);
 int rt_render_gather_async(const rt_scene* scene, const rt_params* params, int tile_rows, const rt_frame* frame,
                            void* hip_stream);
+/* Peer access the gathers use from dst_device to src_device, enabled on
+ * first use per pair: 1 = enabled (copy engines read over xGMI; also the
+ * answer for dst == src), 0 = unavailable or refused by the runtime (e.g.
+ * hipErrorPeerAccessUnsupported) or disabled with the environment variable
+ * RT_PEER_ACCESS=0 -- the gathers then still work, hipMemcpyPeerAsync staging
+ * each copy itself; RT_EINVAL for a device that is not visible.
+ * NOTE: the distinct-device branches (peer enable, cross-device event waits,
+ * xGMI copies) have only run in tests on machines with >= 2 GPUs; the
+ * builder's own GPU box has one, where every slot is device 0. */
+int rt_peer_access(int dst_device, int src_device);
 
 /* ---- instrumentation (roofline accounting, tests) ----------------------- */
 enum {

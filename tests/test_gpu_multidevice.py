@@ -11,6 +11,7 @@ bit for bit, since the Philox stream is keyed by the global pixel.
 import ctypes as C
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -118,3 +119,74 @@ def test_demo_exits_cleanly_without_shutdown(tmp_path):
     p = helpers.params(W, H, 4, 5, chunks=tipe_rt.RT_SPP_CHUNKS_AUTO)
     ref = helpers.oracle_render(helpers.cornell(), p)
     assert out.read_text().split() == helpers.ppm_text(ref["canva"]).split()
+
+
+def test_rt_init_rejects_invisible_device_and_keeps_list():
+    """rt_init with a device id that is not visible returns RT_EINVAL and
+    leaves the previous device list in force (nothing half-committed)."""
+    lib = tipe_rt.lib()
+    n = lib.rt_device_count()
+    assert n >= 1
+    tipe_rt.check(lib.rt_init(1, (C.c_int * 1)(0)))
+    try:
+        for bad in ([0, n], [-1], [n + 7, 0]):
+            assert lib.rt_init(len(bad), (C.c_int * len(bad))(*bad)) == tipe_rt.RT_EINVAL
+            assert b"not visible" in lib.rt_last_error()
+        bundle = helpers.cornell()
+        p = helpers.params(16, 12, 2, 4)
+        canva, _, _ = tipe_rt.render_rows(bundle.scene, p)       # still device 0 alone
+        assert (canva == helpers.oracle_render(bundle, p)["canva"]).all()
+    finally:
+        tipe_rt.check(lib.rt_init(0, None))
+
+
+def test_peer_access_query():
+    lib = tipe_rt.lib()
+    n = lib.rt_device_count()
+    assert lib.rt_peer_access(0, 0) == 1
+    assert lib.rt_peer_access(0, n) == tipe_rt.RT_EINVAL
+    assert lib.rt_peer_access(-1, 0) == tipe_rt.RT_EINVAL
+
+
+def _device_count():
+    try:
+        return tipe_rt.lib().rt_device_count()
+    except Exception:
+        return 0
+
+
+@pytest.mark.parametrize("peer_env", ["1", "0"])
+def test_render_gather_distinct_devices_bitexact(peer_env):
+    """Slots on distinct GPUs: peer enable (or, with RT_PEER_ACCESS=0, the
+    runtime's staged copies), cross-device event waits and xGMI copies.
+    Needs >= 2 GPUs, so it is skipped on the builder's one-GPU box; run in a
+    subprocess so the environment switch applies from the library's first
+    peer call."""
+    if _device_count() < 2:
+        pytest.skip("needs >= 2 visible GPUs (the distinct-device path has not run on the builder's box)")
+    code = r'''
+import ctypes as C, sys
+sys.path[:0] = %r
+import torch, helpers, tipe_rt
+lib = tipe_rt.lib()
+tipe_rt.check(lib.rt_init(2, (C.c_int * 2)(0, 1)))
+bundle = helpers.pyramid_scene()
+W, H = 52, 41
+p = helpers.params(W, H, 8, 6, chunks=4)
+ref = helpers.oracle_render(bundle, p)
+planes = torch.full((4, H, W, 3), -2.0, dtype=torch.float64, device="cuda:0")
+tipe_rt.render_gather_async(bundle.scene, p, 1, *[planes[k].data_ptr() for k in range(4)],
+                            stream=torch.cuda.current_stream().cuda_stream)
+torch.cuda.synchronize()
+got = planes.cpu().numpy()
+ok = all((got[k] == ref[n]).all() for k, n in enumerate(("canva", "albedo", "normal", "radiance")))
+st = lib.rt_peer_access(0, 1)
+print("RESULT", int(ok), st)
+''' % ([os.path.join(ROOT, "tests"), os.path.join(ROOT, "tipe-raytracer_amd")],)
+    env = dict(os.environ, RT_PEER_ACCESS=peer_env)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][-1].split()
+    assert res[1] == "1"
+    if peer_env == "0":
+        assert res[2] == "0"

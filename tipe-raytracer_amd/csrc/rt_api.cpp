@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -619,15 +620,17 @@ int rt_init(int ndev, const int* devices)
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
     if (n < 1) return fail(RT_EDEVICE, "no HIP device");
-    g_devices.clear();
+    std::vector<int> devs;             // committed only when every id is visible
     if (ndev <= 0 || !devices) {
-        g_devices.push_back(0);
+        devs.push_back(0);
     } else {
         for (int i = 0; i < ndev; ++i) {
-            if (devices[i] < 0 || devices[i] >= n) return fail(RT_EINVAL, "device %d of %d", devices[i], n);
-            g_devices.push_back(devices[i]);
+            if (devices[i] < 0 || devices[i] >= n)
+                return fail(RT_EINVAL, "device %d is not visible (%d device%s)", devices[i], n, n == 1 ? "" : "s");
+            devs.push_back(devices[i]);
         }
     }
+    g_devices.swap(devs);
     g_inited = true;
     return RT_OK;
 }
@@ -644,6 +647,7 @@ void rt_shutdown(void)
 }
 
 const char* rt_last_error(void) { return g_err.c_str(); }
+const char* rt_last_render_kernel(void) { return last_render_kernel(); }
 
 const char* rt_version(void)
 {
@@ -969,21 +973,31 @@ int rt_assemble_async(const rt_color* gathered, long long rank_stride, int world
 // process), then the assemble kernel un-permutes them into row order.
 namespace {
 
-void enable_peer(int dst, int src)
+// Peer access of dst to src, enabled once per pair.  Status: 1 = enabled
+// (the copy engines read src over xGMI), 0 = not available, refused
+// (e.g. hipErrorPeerAccessUnsupported) or switched off with the environment
+// variable RT_PEER_ACCESS=0; hipMemcpyPeerAsync then stages the copy through
+// the host itself, so the gather still works, only slower.
+std::mutex g_peer_mu;
+std::vector<std::array<int, 3>> g_peer;      // (dst, src, status)
+
+int enable_peer(int dst, int src)
 {
-    if (dst == src) return;
-    static std::mutex mu;
-    static std::vector<std::pair<int, int>> done;
-    std::lock_guard<std::mutex> lk(mu);
-    for (auto& d : done)
-        if (d.first == dst && d.second == src) return;
+    if (dst == src) return 1;
+    std::lock_guard<std::mutex> lk(g_peer_mu);
+    for (auto& d : g_peer)
+        if (d[0] == dst && d[1] == src) return d[2];
+    int status = 0;
+    const char* env = std::getenv("RT_PEER_ACCESS");
     int can = 0;
-    if (hipDeviceCanAccessPeer(&can, dst, src) == hipSuccess && can) {
+    if (!(env && env[0] == '0') && hipDeviceCanAccessPeer(&can, dst, src) == hipSuccess && can) {
         DeviceGuard g(dst);
         const hipError_t e = hipDeviceEnablePeerAccess(src, 0);
-        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+        if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) status = 1;
+        (void)hipGetLastError();     // a refusal must not poison the next call's error check
     }
-    done.emplace_back(dst, src);     // without peer access the runtime stages the copy itself
+    g_peer.push_back({dst, src, status});
+    return status;
 }
 
 // One plane: slot r's rows_per_rank*W colours (device src_dev[r]) into the
@@ -1016,6 +1030,14 @@ int check_gather_geometry(int world, int tile_rows, int rows_per_rank, int W, in
 }
 
 }  // namespace
+
+int rt_peer_access(int dst_device, int src_device)
+{
+    const int n = rt_device_count();
+    if (dst_device < 0 || dst_device >= n || src_device < 0 || src_device >= n)
+        return fail(RT_EINVAL, "peer pair %d <- %d: %d visible device%s", dst_device, src_device, n, n == 1 ? "" : "s");
+    return enable_peer(dst_device, src_device);
+}
 
 int rt_gather_async(int world, const int* src_devices, const rt_color* const* locals, int tile_rows,
                     int rows_per_rank, int W, int H, int dst_device, rt_color* out, void* hip_stream)
@@ -1128,14 +1150,24 @@ int rt_render_gather_async(const rt_scene* scene, const rt_params* params, int t
         }
         if (staging) (void)hipFreeAsync(staging, dst_st);
         if (rc == RT_OK) {
-            const hipError_t e = hipEventRecord(go, dst_st);     // reused: "the copies are done"
-            for (int q = 0; q < G && e == hipSuccess; ++q) {
+            // the slots free their planes only after the copies that read them
+            hipError_t e = hipEventRecord(go, dst_st);            // reused: "the copies are done"
+            if (e != hipSuccess) rc = fail(RT_EDEVICE, "gather event: %s", hipGetErrorString(e));
+            for (int q = 0; q < G && rc == RT_OK; ++q) {
                 DeviceGuard gq(devs[(size_t)q]);
-                (void)hipStreamWaitEvent(slots[(size_t)q].ps->st, go, 0);
+                if ((e = hipStreamWaitEvent(slots[(size_t)q].ps->st, go, 0)) != hipSuccess)
+                    rc = fail(RT_EDEVICE, "device %d wait: %s", devs[(size_t)q], hipGetErrorString(e));
             }
         }
     }
-    if (rc != RT_OK) {               // keep the error message; make every slot idle before freeing
+    if (rc != RT_OK) {
+        // Keep the error message.  Copies already queued on the destination's
+        // stream may still read slot planes, and the slots may still render
+        // into them: drain both before release() hands the memory back.
+        {
+            DeviceGuard g(dst);
+            (void)hipStreamSynchronize(dst_st);
+        }
         for (auto& s : slots)
             if (s.ps) {
                 DeviceGuard gq(s.ps->device);

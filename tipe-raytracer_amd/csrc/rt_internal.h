@@ -129,6 +129,8 @@ struct UniBlock { double v[U_COUNT]; };
 // launchers (rt_kernels.hip)
 int launch_set_uniforms(const UniBlock& u, double* d_uni, void* stream);
 int launch_render(const KParams& kp, void* stream);
+// Name of the render kernel the calling thread's last launch_render chose.
+const char* last_render_kernel();
 int launch_count(const KParams& kp, void* stream);
 int launch_assemble(const double* gathered, long long rank_stride, int world, int tile_rows,
                     int rows_per_rank, int W, int H, double* out, void* stream);

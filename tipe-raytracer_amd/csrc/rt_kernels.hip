@@ -406,7 +406,7 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
         asm volatile("" : "+v"(g.ax), "+v"(g.ay), "+v"(g.az), "+v"(g.abx), "+v"(g.aby), "+v"(g.abz), "+v"(g.acx),
                      "+v"(g.acy), "+v"(g.acz), "+v"(g.nx), "+v"(g.ny), "+v"(g.nz));
     } else {
-        g = O32 ? *(const TriGeo*)((const char*)kp.tri + (uint32_t)k * (uint32_t)sizeof(TriGeo)) : kp.tri[k];
+        g = kp.tri[k];
     }
     const double det = -(d.x * g.nx + d.y * g.ny + d.z * g.nz);
     if (det >= 1E-6) {
@@ -3041,19 +3041,30 @@ static void queue_launch(bool sky, bool ao, unsigned nb, hipStream_t st, const K
 static unsigned qdiv_magic(unsigned d) { return d ? (unsigned)(0xffffffffull / d) : 0u; }
 #endif
 
+static thread_local const char* t_last_kernel = "none";
+const char* last_render_kernel() { return t_last_kernel; }
+
 int launch_render(const KParams& kp, void* stream)
 {
 #if RT_QUEUE > 0
-    // (the deep-tree instantiation walks kp.bvhh: a tree without the 64-byte
-    // form renders with the fixed-grid kernel)
-    const bool qbvh = kp.bvh != nullptr && kp.bvh_stack <= kStackQ && (!RT_QNODE_H || kp.bvhh != nullptr);
+    // Node visits per lane and round: 4 for shallow trees (128-byte nodes,
+    // kp.bvh), 3 for deep ones (kp.bvh_steps, host; compile-time per
+    // instantiation).  The deep-tree instantiation walks the 64-byte nodes
+    // kp.bvhh: a deep tree that pack_bvh_h refused (a coordinate beyond
+    // binary16's range, a leaf index above 65535, an oversized leaf) renders
+    // with the fixed-grid kernel; a shallow one keeps the queue kernel.
+    int qb = 0;
+    bool qbvh = false;
+    if (kp.bvh != nullptr && kp.bvh_stack <= kStackQ) {
+        qb = kp.bvh_steps <= 3 || kp.bvh_stack > kStackQ4 ? 3 : 4;
+        qbvh = qb == 4 || !RT_QNODE_H || kp.bvhh != nullptr;
+    }
     if (kp.task_ctr && kp.chunks > 1 && (!kp.bvh || qbvh) && !kp.cuda && !kp.f32 && !kp.sums) {
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
-        // node visits per lane and round: 4 for shallow trees, 3 for deep ones
-        // (kp.bvh_steps, host; compile-time per instantiation)
-        const int qb = qbvh ? (kp.bvh_steps <= 3 || kp.bvh_stack > kStackQ4 ? 3 : 4) : 0;
+        if (!qbvh) qb = 0;
+        t_last_kernel = qb == 3 ? "render_kernel_q<QB=3>" : qb == 4 ? "render_kernel_q<QB=4>" : "render_kernel_q<QB=0>";
         const unsigned nb = queue_grid(sky, ao, qb);
         unsigned long long* tr = nullptr;
         const char* tf = std::getenv("RT_QUEUE_TRACE");
@@ -3083,7 +3094,11 @@ int launch_render(const KParams& kp, void* stream)
         }
     } else
 #endif
-    launch_variant<false>(kp, stream);
+    {
+        launch_variant<false>(kp, stream);
+        t_last_kernel = kp.f32 ? "render_kernel_f32" : kp.cuda ? "render_kernel_cuda" : kp.bvh ? "render_kernel<BVH>"
+                                                                                                 : "render_kernel";
+    }
     if (kp.chunks > 1) {
         const long long npx = (long long)kp.band_rows * kp.W;
         long long blocks = (npx + 255) / 256;

@@ -49,6 +49,7 @@ def lib():
         L.rt_init.argtypes = [C.c_int, P(C.c_int)]
         L.rt_last_error.restype = C.c_char_p
         L.rt_version.restype = C.c_char_p
+        L.rt_last_render_kernel.restype = C.c_char_p
         L.rt_render_rows.argtypes = [P(Scene), P(Params), C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.rt_fill_canva.argtypes = [C.c_void_p]
         L.rt_fill_canva.restype = C.c_void_p
@@ -61,6 +62,7 @@ def lib():
         L.rt_gather_async.argtypes = [C.c_int, P(C.c_int), P(C.c_void_p), C.c_int, C.c_int, C.c_int, C.c_int,
                                       C.c_int, C.c_void_p, C.c_void_p]
         L.rt_render_gather_async.argtypes = [P(Scene), P(Params), C.c_int, P(Frame), C.c_void_p]
+        L.rt_peer_access.argtypes = [C.c_int, C.c_int]
         L.rt_selftest_math.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         L.rt_verify_sampler_phi.argtypes = [C.c_ulonglong, C.c_ulonglong, C.c_void_p]
         L.rt_verify_sphere_pass.argtypes = [P(Scene), C.c_void_p, C.c_longlong, C.c_void_p]
@@ -90,7 +92,8 @@ EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error",
                     "rt_selftest_math", "rt_accumulate_async", "rt_resolve_async", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
                     "rt_denoise_unpack", "rt_denoise_pack_async", "rt_verify_sampler_phi",
                     "rt_verify_sphere_pass", "rt_verify_normalize", "rt_set_zero_throughput_exit", "rt_set_fill_spp_chunks", "rt_set_fill_precision",
-                    "rt_scene_cache_clear", "rt_gather_async", "rt_render_gather_async"]
+                    "rt_scene_cache_clear", "rt_gather_async", "rt_render_gather_async", "rt_peer_access",
+                    "rt_last_render_kernel"]
 
 # rt_denoise_fn (rt.h): denoiser()'s signature, denoiser.h:31
 DENOISE_FN = C.CFUNCTYPE(None, C.c_int, C.c_int, C.c_void_p, Camera, C.c_void_p, C.c_void_p)
@@ -143,6 +146,11 @@ def denoise_unpack(color3):
     c = np.ascontiguousarray(color3, dtype=np.float32)
     check(lib().rt_denoise_unpack(W, H, c.ctypes.data, out.ctypes.data))
     return out
+
+
+def last_render_kernel():
+    """rt_last_render_kernel: the render kernel this thread's last launch used."""
+    return lib().rt_last_render_kernel().decode()
 
 
 def check(rc):

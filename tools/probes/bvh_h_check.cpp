@@ -31,7 +31,7 @@ int main()
     std::vector<BvhNodeH> h;
     float rbox = 0;
     if (!pack_bvh_h(b.nodes4, h, rbox)) {      // does not fit binary16: the kernel keeps 128-byte nodes
-        std::printf("{\"nodes\": %zu, \"packed\": false}\n", b.nodes4.size());
+        std::printf("{\"nodes\": %zu, \"packed\": false, \"depth4\": %d}\n", b.nodes4.size(), b.depth4);
         return 0;
     }
     long bad = 0;
