@@ -121,7 +121,9 @@ typedef struct rt_params {
  * branch: when the last sphere is the closest hit, its emissionColor becomes
  * the sky texel sphere_uvmapping (texture.h:92-112) picks and its alpha 1. */
 /* rt_params.precision.  FP64 (default) is the reference's arithmetic, in its
- * operation order: images equal the CPU oracle's bit for bit.  FP32 runs the
+ * operation order: images equal the CPU oracle's bit for bit.  FP32 is
+ * EXPERIMENTAL (measured 1.1-3.4e-4 per-channel RMSE against the oracle's
+ * FP64 frames, above north_star's 1e-4; frozen, never the benchmark): it runs the
  * same integrator (main.c semantics, same Philox draws and draw order) in
  * binary32 -- ray/sphere (stable roots), ray/triangle, sampler, shading --
  * with the per-pixel sums and the resolve kept in fp64.  It is NOT bit-exact:

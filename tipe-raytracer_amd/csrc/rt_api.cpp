@@ -651,7 +651,8 @@ const char* rt_last_render_kernel(void) { return last_render_kernel(); }
 
 const char* rt_version(void)
 {
-    return "tipe-raytracer-mi355x 0.3 (abi 2, gfx950; precision FP64 bit-exact by default, opt-in RT_PREC_FP32; "
+    return "tipe-raytracer-mi355x 0.4 (abi 2, gfx950; precision FP64 bit-exact by default; RT_PREC_FP32 is "
+           "EXPERIMENTAL: not bit-exact and above north_star's 1e-4 per-channel RMSE (1.1-3.4e-4); "
            "rt_params_init defaults spp_chunks to RT_SPP_CHUNKS_AUTO, a fixed per-pixel slice grouping)";
 }
 
@@ -676,6 +677,8 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
 
     // Spheres padded to an even count with never-hit records (r2 = -inf makes
     // the discriminant -inf): the kernel reads them two per s_load_dwordx16.
+    // the candidate pass keeps the winner's slot in 16 mantissa bits (RT_CAND_TAG)
+    if (scene->nbSpheres > 65534) return fail(RT_EUNSUPPORTED, "%d spheres > 65534", scene->nbSpheres);
     const int ns_pad = (scene->nbSpheres + 1) & ~1;
     std::vector<SphGeo> sph((size_t)ns_pad, SphGeo{0.0, 0.0, 0.0, -HUGE_VAL});
     std::vector<SphCand> cand((size_t)ns_pad, SphCand{0.0, 0.0, 0.0, HUGE_VAL});

@@ -64,6 +64,9 @@
 #endif
 static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x1p-20,
               "candidate half-width M must be >= 8 x the sqrt error bound 2^-47.2/sqrt(T1)");
+#ifndef RT_CAND_TAG                 // candidate pass: the running best carries its sphere slot in the low
+#define RT_CAND_TAG 1               // 16 mantissa bits (spheres_closest), so no separate index select
+#endif
 #ifndef RT_AO_FIRST                 // AO scenes: the AO direction before the bounce direction (ROLE_AO)
 #define RT_AO_FIRST 1
 #endif
@@ -292,6 +295,17 @@ __device__ __forceinline__ int spheres_exact_scan(const KParams& kp, const V3 o,
 // a strictly smaller t_ref (the reference keeps the first of equal t).
 // Non-finite o, d or Hs^2 > 2^1000 make the ray ambiguous up front.
 // CU (main_cuda.cu's thresholds): t1 >= 0, t2 >= 0.001, one interval pair each.
+// The candidate's n with its low 16 mantissa bits replaced by sphere slot k:
+// one v_and_or_b32 with the mask in a VGPR (msk, loop-invariant; a literal
+// would split it into v_and + v_or) and the wave-uniform slot as its one
+// scalar operand.
+__device__ __forceinline__ double cand_tag(double n, int k, uint32_t msk)
+{
+    uint32_t lo;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(lo) : "v"((uint32_t)__double2loint(n)), "v"(msk), "s"(k));
+    return __hiloint2double(__double2hiint(n), (int)lo);
+}
+
 template <bool COUNT, bool CU, bool AMGM = false>
 __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, const V3 d, double a, double two_a,
                                                double four_a, bool fast, double rc2a, double& t_best, Cnt& cnt)
@@ -322,6 +336,8 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     int bk = -1;
     // finite o, d, Hs^2 keep every D below finite; anything else takes the exact scan
     bool amb = !(fast && Hs2 <= 0x1p1000);
+    uint32_t msk = 0xffff0000u;
+    asm volatile("" : "+v"(msk));
     for (int k = 0; k < kp.ns_pad; k += 2) {
         double g[8];
 #pragma unroll
@@ -351,13 +367,18 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             const bool sure = n >= tP;
             amb = amb || (valid && (sure != (n >= tM)));    // the chosen root straddles 1e-4
             const bool cand = valid && sure;
-            const double diff = n - bn;
+            // RT_CAND_TAG: n with its low 16 mantissa bits replaced by the slot
+            // (one v_and_or_b32; host: ns_pad <= 65536); |nt - n| < 2^-36 |n|
+            // <= 2^-34.4 Hs, inside M's slack
+            const double nt = RT_CAND_TAG ? cand_tag(n, k + e, msk) : n;
+            const double diff = nt - bn;
             const bool closer = cand && diff < -M2;
             amb = amb || (cand && fabs(diff) <= M2);        // (closer implies |diff| > M2)
-            bn = closer ? n : bn;
-            bk = closer ? k + e : bk;
+            bn = closer ? nt : bn;
+            if (!RT_CAND_TAG) bk = closer ? k + e : bk;
         }
     }
+    if (RT_CAND_TAG) bk = bn < INF ? (int)((uint32_t)__double2loint(bn) & 0xffffu) : -1;
     if (COUNT)
         for (int k = 0; k < kp.ns; ++k) cnt.c[RT_CNT_SPHERE_DISC] += disc_positive(kp.sph[k], o, d, four_a) ? 1 : 0;
     double t = INF;
