@@ -158,7 +158,7 @@ def cpu_baseline(scene, cam, threads=12):
 CONFIGS = {
     # name: (scene builder, spp measured, bounces, useAO, W, H, full spp, GPUs of the config)
     # C3/C4/C5 are timed at their FULL spp on the full frame with spp_chunks AUTO
-    # (P = 32, tapered slices: rt.h rt_chunk_bound), i.e. exactly the tasks the
+    # (tapered slices: rt.h rt_chunk_bound), i.e. exactly the tasks the
     # config's own frame hands out (C4: ~67 samples per slice, C5: ~167); the
     # sweep scene is defined at 64 spp.
     "C3": ("pyramid", 1000, 6, False, 1200, 900, 1000, 1),
@@ -193,10 +193,10 @@ def work_flops(c, ns):
 def task_regime(spp, w, h):
     """The (chunk, pixel) tasks one launch hands out: rt_chunk_bound's slices."""
     P = tipe_rt.types.rt_resolve_spp_chunks(tipe_rt.RT_SPP_CHUNKS_AUTO, spp)
-    taper = not (P < 5 or spp < 8 * P)
-    den = 8 * (P - 3) + 7 if taper else P
-    main = spp * 8 / den if taper else spp / P
-    return {"spp_chunks": P, "tapered": taper, "samples_per_main_slice": round(main, 1),
+    L = tipe_rt.types.rt_chunk_taper_levels(spp, P)
+    den = (P - L) * (1 << L) + (1 << L) - 1 if L else P
+    main = spp * (1 << L) / den if L else spp / P
+    return {"spp_chunks": P, "tapered": bool(L), "taper_levels": L, "samples_per_main_slice": round(main, 1),
             "tasks": w * h * P}
 
 

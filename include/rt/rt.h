@@ -160,17 +160,28 @@ static inline int rt_resolve_spp_chunks(int spp_chunks, int spp)
 }
 
 /* Slice c (0 <= c < P) of a pixel's S samples is [rt_chunk_bound(c),
- * rt_chunk_bound(c + 1)).  P equal slices (c*S/P) when P < 5 or S < 8*P;
- * otherwise P - 3 equal slices followed by three tapered ones, weights
- * 8, ..., 8, 4, 2, 1: the task-queue kernel hands out slices in order, so
- * the tasks still running when its queue empties are short (the frame's
- * tail).  A pure function of (c, S, P), shared by the kernels and the
- * oracle, so images stay independent of GPU count and tiling. */
+ * rt_chunk_bound(c + 1)).  Equal slices (c*S/P) when P < 5 or S < 8*P;
+ * otherwise E = P - L equal slices of weight 2^L followed by L tapered ones
+ * of weights 2^(L-1), ..., 2, 1, with L = 5 taper levels when P >= 12 and
+ * S >= 32*P, else L = 3 (weights 8, ..., 8, 4, 2, 1).  The task-queue kernel
+ * hands out slices in order, so the tasks still running when its queue
+ * empties are short (the frame's tail); five levels keep that tail as fine
+ * with 12 slices as three levels do with 32, i.e. with 2.7x fewer partial
+ * sums per pixel.  A pure function of (c, S, P), shared by the kernels and
+ * the oracle, so images stay independent of GPU count and tiling. */
+static inline int rt_chunk_taper_levels(long long S, long long P)
+{
+    if (P >= 12 && S >= 32 * P) return 5;
+    if (P >= 5 && S >= 8 * P) return 3;
+    return 0;
+}
 static inline long long rt_chunk_bound(long long c, long long S, long long P)
 {
-    if (P < 5 || S < 8 * P) return c * S / P;
-    const long long U = 8 * (P - 3) + 7;
-    const long long w = c <= P - 3 ? 8 * c : c == P - 2 ? 8 * (P - 3) + 4 : c == P - 1 ? 8 * (P - 3) + 6 : U;
+    const int L = rt_chunk_taper_levels(S, P);
+    if (!L) return c * S / P;
+    const long long one = 1LL << L, E = P - L;
+    const long long U = E * one + (one - 1);
+    const long long w = c <= E ? one * c : one * E + one - (one >> (c - E));
     return w * S / U;
 }
 

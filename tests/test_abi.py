@@ -148,8 +148,8 @@ CHUNK_C = r"""
 #include <stdio.h>
 #include "rt/rt.h"
 int main(void) {
-  const int S[] = {1, 2, 7, 8, 39, 40, 100, 1000, 2000, 5000, 1 << 30};
-  const int P[] = {1, 2, 4, 5, 6, 8, 16, 32, 64};
+  const int S[] = {1, 2, 7, 8, 39, 40, 100, 383, 384, 1000, 2000, 5000, 1 << 30};
+  const int P[] = {1, 2, 4, 5, 6, 8, 11, 12, 13, 16, 32, 64};
   for (unsigned i = 0; i < sizeof S / sizeof S[0]; ++i)
     for (unsigned j = 0; j < sizeof P / sizeof P[0]; ++j) {
       int p = rt_resolve_spp_chunks(P[j], S[i]);
@@ -179,8 +179,14 @@ def test_chunk_bounds_header_matches_mirror(tmp_path):
         assert bs[0] == 0 and bs[-1] == S and len(bs) == P + 1
         sizes = [bs[c + 1] - bs[c] for c in range(P)]
         assert min(sizes) >= 1, (S, P, sizes)
-        if P >= 5 and S >= 8 * P:
-            full = sizes[:P - 3]
+        L = T.rt_chunk_taper_levels(S, P)
+        assert L == (5 if P >= 12 and S >= 32 * P else 3 if P >= 5 and S >= 8 * P else 0)
+        if L:
+            full = sizes[:P - L]
             assert max(full) - min(full) <= 1
-            assert sizes[-3] < min(full) and sizes[-2] < sizes[-3] and sizes[-1] <= sizes[-2]
-    assert T.rt_chunk_bound(29, 1000, 32) == 970 and T.rt_chunk_bound(31, 1000, 32) == 995
+            tail = sizes[P - L:]
+            assert tail[0] < min(full) and all(b <= a for a, b in zip(tail, tail[1:])), (S, P, sizes)
+            assert tail[-1] * (1 << L) <= min(full) + (1 << L), (S, P, sizes)   # about 2^-L of a full slice
+    assert T.rt_chunk_bound(29, 1000, 32) == 970 and T.rt_chunk_bound(31, 1000, 32) == 995   # L = 3
+    # L = 5 at 12 slices: 7 x 125.5, then 62.7, 31.4, 15.7, 7.8, 3.9 samples
+    assert [T.rt_chunk_bound(c, 1000, 12) for c in (7, 8, 11, 12)] == [878, 941, 996, 1000]

@@ -322,8 +322,10 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.key0 = (uint32_t)p->seed;
     kp.key1 = (uint32_t)(p->seed >> 32);
     kp.chunks = rt_resolve_spp_chunks(p->spp_chunks, p->nbRayonParPixel);
-    kp.chunk_taper = !(kp.chunks < 5 || (long long)kp.S < 8ll * kp.chunks);
-    kp.chunk_den = kp.chunk_taper ? 8u * (unsigned)(kp.chunks - 3) + 7u : (unsigned)kp.chunks;
+    kp.chunk_taper = rt_chunk_taper_levels(kp.S, kp.chunks);      // rt.h rt_chunk_bound
+    kp.chunk_den = kp.chunk_taper ? (unsigned)(kp.chunks - kp.chunk_taper) * (1u << kp.chunk_taper) +
+                                        ((1u << kp.chunk_taper) - 1u)
+                                  : (unsigned)kp.chunks;
     kp.row_base = t->row_base;
     kp.tile_rows = t->tile_rows;
     kp.tile_first = t->tile_first;

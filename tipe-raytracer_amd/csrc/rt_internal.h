@@ -102,8 +102,8 @@ struct KParams {
     int cam_pin;             // aperture 0 and no -0 camera coordinate: co + (jx*0, jy*0, 0) == co exactly
     uint32_t key0, key1;
     int chunks;              // samples of a pixel split into this many chunks
-    int chunk_taper;         // rt_chunk_bound's tapered slices (else equal ones)
-    unsigned chunk_den;      // rt_chunk_bound's divisor: chunks, or 8 (chunks - 3) + 7 tapered
+    int chunk_taper;         // rt_chunk_bound's taper levels L (0: equal slices)
+    unsigned chunk_den;      // rt_chunk_bound's divisor: chunks, or (chunks - L) 2^L + 2^L - 1 tapered
     // tiling
     int row_base, tile_rows, tile_first, tile_step, n_tiles, row_end;
     int local_rows;          // n_tiles * tile_rows

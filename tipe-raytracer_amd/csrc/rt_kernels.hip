@@ -1633,14 +1633,14 @@ __device__ __forceinline__ unsigned udiv_q(unsigned n, unsigned d, unsigned m, u
 }
 
 // First sample of chunk c, rt.h rt_chunk_bound: w(c)*S/den with w(c) = c
-// (den = P) or the tapered weights (den = 8 (P - 3) + 7); 32-bit magic
+// (den = P) or the tapered weights (den = (P - L) 2^L + 2^L - 1); 32-bit magic
 // division when (den + 1) * S < 2^32 (qm_chunks != 0), else 64-bit.
 __device__ __forceinline__ int chunk_start(int S, int chunks, int taper, unsigned den, unsigned qm_chunks, unsigned c)
 {
     unsigned w = c;
-    if (taper) {
-        const unsigned P = (unsigned)chunks;
-        w = c + 3u <= P ? 8u * c : c + 2u == P ? 8u * (P - 3u) + 4u : c + 1u == P ? 8u * (P - 3u) + 6u : den;
+    if (taper) {                     // L = taper levels: weights 2^L x E, then 2^(L-1) .. 1
+        const unsigned E = (unsigned)chunks - (unsigned)taper, one = 1u << taper;
+        w = c <= E ? c << taper : (E << taper) + one - (one >> (c - E));
     }
     if (qm_chunks != 0u) {
         unsigned r;

@@ -13,14 +13,27 @@ def rt_resolve_spp_chunks(spp_chunks, spp):
     return 1 if (p <= 1 or spp <= 1) else min(p, spp)
 
 
+def rt_chunk_taper_levels(S, P):
+    """rt.h rt_chunk_taper_levels: 5 (P >= 12, S >= 32 P), 3 (P >= 5, S >= 8 P) or 0."""
+    if P >= 12 and S >= 32 * P:
+        return 5
+    if P >= 5 and S >= 8 * P:
+        return 3
+    return 0
+
+
 def rt_chunk_bound(c, S, P):
     """rt.h rt_chunk_bound: first sample of slice c of S samples in P slices
-    (equal slices, or P - 3 equal ones then three tapered, weights 8..8, 4, 2, 1)."""
-    if P < 5 or S < 8 * P:
+    (equal slices, or P - L equal ones of weight 2^L then L tapered, weights
+    2^(L-1) .. 1)."""
+    L = rt_chunk_taper_levels(S, P)
+    if not L:
         return c * S // P
-    U = 8 * (P - 3) + 7
-    w = 8 * c if c <= P - 3 else 8 * (P - 3) + 4 if c == P - 2 else 8 * (P - 3) + 6 if c == P - 1 else U
+    one, E = 1 << L, P - L
+    U = E * one + one - 1
+    w = one * c if c <= E else one * E + one - (one >> (c - E))
     return w * S // U
+
 
 (RT_CNT_SAMPLES, RT_CNT_CASTS, RT_CNT_SPHERE_TESTS, RT_CNT_SPHERE_DISC,
  RT_CNT_TRI_TESTS, RT_CNT_SHADE, RT_CNT_TEX_HITS, RT_CNT_REFRACT,
