@@ -610,8 +610,12 @@ def main():
         if rank == 0:
             ndev = torch.cuda.device_count()
             devs = [r if args.dist_backend == "nccl" else r % max(1, ndev) for r in range(world)]
-            single = single_process_leg(scene, p, world, devs, max(1, min(args.steps, 5)),
-                                        None if ref is None else ref[0])
+            try:
+                single = single_process_leg(scene, p, world, devs, max(1, min(args.steps, 5)),
+                                            None if ref is None else ref[0])
+            except Exception as e:       # reported, never fatal to the RCCL measurement above
+                single = {"error": repr(e), "devices": devs}
+                print("single_process leg failed: %r" % e, file=sys.stderr)
             if single.get("verified_vs_single_device") is False:
                 print("verify: rt_render_gather_async frame differs from the single-device frame", file=sys.stderr)
         dist.barrier(group=cpu_group)
