@@ -162,7 +162,7 @@ static inline int rt_resolve_spp_chunks(int spp_chunks, int spp)
 /* Slice c (0 <= c < P) of a pixel's S samples is [rt_chunk_bound(c),
  * rt_chunk_bound(c + 1)).  Equal slices (c*S/P) when P < 5 or S < 8*P;
  * otherwise E = P - L equal slices of weight 2^L followed by L tapered ones
- * of weights 2^(L-1), ..., 2, 1, with L = 5 taper levels when P >= 12 and
+ * of weights 2^(L-1), ..., 2, 1, with L = 5 taper levels when P >= 8 and
  * S >= 32*P, else L = 3 (weights 8, ..., 8, 4, 2, 1).  The task-queue kernel
  * hands out slices in order, so the tasks still running when its queue
  * empties are short (the frame's tail); five levels keep that tail as fine
@@ -171,7 +171,7 @@ static inline int rt_resolve_spp_chunks(int spp_chunks, int spp)
  * the oracle, so images stay independent of GPU count and tiling. */
 static inline int rt_chunk_taper_levels(long long S, long long P)
 {
-    if (P >= 12 && S >= 32 * P) return 5;
+    if (P >= 8 && S >= 32 * P) return 5;
     if (P >= 5 && S >= 8 * P) return 3;
     return 0;
 }

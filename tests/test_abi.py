@@ -180,7 +180,7 @@ def test_chunk_bounds_header_matches_mirror(tmp_path):
         sizes = [bs[c + 1] - bs[c] for c in range(P)]
         assert min(sizes) >= 1, (S, P, sizes)
         L = T.rt_chunk_taper_levels(S, P)
-        assert L == (5 if P >= 12 and S >= 32 * P else 3 if P >= 5 and S >= 8 * P else 0)
+        assert L == (5 if P >= 8 and S >= 32 * P else 3 if P >= 5 and S >= 8 * P else 0)
         if L:
             full = sizes[:P - L]
             assert max(full) - min(full) <= 1

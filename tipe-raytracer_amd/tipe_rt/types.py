@@ -14,8 +14,8 @@ def rt_resolve_spp_chunks(spp_chunks, spp):
 
 
 def rt_chunk_taper_levels(S, P):
-    """rt.h rt_chunk_taper_levels: 5 (P >= 12, S >= 32 P), 3 (P >= 5, S >= 8 P) or 0."""
-    if P >= 12 and S >= 32 * P:
+    """rt.h rt_chunk_taper_levels: 5 (P >= 8, S >= 32 P), 3 (P >= 5, S >= 8 P) or 0."""
+    if P >= 8 and S >= 32 * P:
         return 5
     if P >= 5 and S >= 8 * P:
         return 3

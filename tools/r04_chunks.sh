@@ -12,12 +12,12 @@ fi
 timeout -k 10 120 tools/probes/op_rates3 > $O/op_rates3.txt 2>&1 && grep "waves/SIMD 8" $O/op_rates3.txt
 timeout -k 10 120 tools/probes/split_traffic > $O/split_traffic.json 2>&1 && cat $O/split_traffic.json
 for r in 1 2; do
-  for c in 32 12; do
+  for c in 32 16 12 8; do
     timeout -k 10 200 python bench.py --steps 8 --warmup 2 --no-extras --no-cpu-baseline --chunks $c > $O/bench_c${c}_r$r.json 2>> $O/bench.err || { tail -5 $O/bench.err; exit 1; }
     python3 -c "import json; d=json.load(open('$O/bench_c${c}_r$r.json')); print('bench chunks $c round $r', d['value'], d['roofline']['kernel_ms'])"
   done
 done
-for c in 32 12; do
+for c in 32 16 12 8; do
   timeout -k 10 300 python tools/rank_share_rate.py --chunks $c --pipeline --tile-rows 1 > $O/share_c$c.jsonl 2>> $O/share.err || { tail -5 $O/share.err; exit 1; }
   echo "share chunks $c"; cat $O/share_c$c.jsonl
 done
