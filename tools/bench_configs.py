@@ -39,7 +39,7 @@ CONFIGS = {
 }
 
 
-def run(name, spp_scale, dev, stream, spp_override=0):
+def run(name, spp_scale, dev, stream, spp_override=0, chunks=None):
     mesh_fn, spp, bounces, ao, ao_int, full_spp, W, H, gpus = CONFIGS[name]
     spp = spp_override or max(1, int(spp * spp_scale))
     spheres = scenes.cornell_spheres()
@@ -55,7 +55,8 @@ def run(name, spp_scale, dev, stream, spp_override=0):
         scene = tipe_rt.make_scene(spheres, tris, qm, mats, tw, th, nm)
         nt = len(tris)
     cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
-    p = tipe_rt.make_params(W, H, spp, bounces, cam, focus=3.0, use_ao=ao, ao=ao_int, chunks=tipe_rt.RT_SPP_CHUNKS_AUTO)
+    p = tipe_rt.make_params(W, H, spp, bounces, cam, focus=3.0, use_ao=ao, ao=ao_int,
+                            chunks=tipe_rt.RT_SPP_CHUNKS_AUTO if chunks is None else chunks)
     ds = tipe_rt.DeviceScene(scene, dev.index)
     tiling = tipe_rt.band_tiling(0, H - 1)
     out = torch.empty((3, H, W, 3), dtype=torch.float64, device=dev)
@@ -88,7 +89,7 @@ def run(name, spp_scale, dev, stream, spp_override=0):
             "ao": ao, "spp_measured": spp, "kernel_ms": round(ms, 3), "wall_ms": round(wall * 1e3, 3),
             "kernel_msamples_per_s": round(rate, 3),
             "full_frame_s_at_config_spp": round(W * H * full_spp / (rate * 1e6), 2),
-            "config_gpus": gpus,
+            "config_gpus": gpus, "spp_chunks": tipe_rt.types.rt_resolve_spp_chunks(p.spp_chunks, spp),
             "full_frame_s_on_config_gpus_linear": round(W * H * full_spp / (rate * 1e6) / gpus, 2),
             "events_per_sample": {k: round(cnt[i] / max(cnt[0], 1), 7) for i, k in enumerate(tipe_rt.COUNTER_NAMES)}}
 
@@ -98,12 +99,15 @@ def main():
     ap.add_argument("--spp-scale", type=float, default=1.0)
     ap.add_argument("--only", default=",".join(CONFIGS))
     ap.add_argument("--spp", type=int, default=0, help="spp of every config (default: the table's, x --spp-scale)")
+    ap.add_argument("--chunks", type=int, default=None, help="rt_params.spp_chunks (default RT_SPP_CHUNKS_AUTO)")
+    ap.add_argument("--full-spp", action="store_true", help="each config at its full spp")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
     for name in args.only.split(","):
-        print(json.dumps(run(name, args.spp_scale, dev, stream, args.spp)), flush=True)
+        spp = CONFIGS[name][5] if args.full_spp else args.spp
+        print(json.dumps(run(name, args.spp_scale, dev, stream, spp, args.chunks)), flush=True)
 
 
 if __name__ == "__main__":
