@@ -67,7 +67,10 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_CAND_TAG                 // candidate pass: the running best carries its sphere slot in the low
 #define RT_CAND_TAG 1               // 16 mantissa bits (spheres_closest), so no separate index select
 #endif
-#ifndef RT_AO_FIRST                 // AO scenes: the AO direction before the bounce direction (ROLE_AO)
+#ifndef RT_CAND_MIN2                // candidate pass: min and second min of the tagged candidates, one
+#define RT_CAND_MIN2 0              // ambiguity test after the scan (A/B knob)
+#endif
+#ifndef RT_AO_FIRST               // AO scenes: the AO direction before the bounce direction (ROLE_AO)
 #define RT_AO_FIRST 1
 #endif
 #ifndef RT_QTASK_TABLE              // sphere-scene queue kernel: tasks decoded per batch into LDS (A/B knob;
@@ -306,6 +309,22 @@ __device__ __forceinline__ double cand_tag(double n, int k, uint32_t msk)
     return __hiloint2double(__double2hiint(n), (int)lo);
 }
 
+// v_min_f64 / v_max_f64 of two finite, non-NaN operands (the candidate
+// pass's tagged values): fmin/fmax would first canonicalize the bit-built
+// operand (an extra v_max_f64 x, x each).
+__device__ __forceinline__ double dmin_raw(double a, double b)
+{
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double dmax_raw(double a, double b)
+{
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 template <bool COUNT, bool CU, bool AMGM = false>
 __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, const V3 d, double a, double two_a,
                                                double four_a, bool fast, double rc2a, double& t_best, Cnt& cnt)
@@ -338,6 +357,12 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     bool amb = !(fast && Hs2 <= 0x1p1000);
     uint32_t msk = 0xffff0000u;
     asm volatile("" : "+v"(msk));
+    // RT_CAND_MIN2: the smallest and second-smallest tagged candidate (bn, bn2;
+    // non-candidates enter as a finite sentinel above 2^1000 that keeps the
+    // tag), ambiguity decided once after the scan (bn2 - bn <= 2M)
+    constexpr bool MN = RT_CAND_MIN2 && !CU;
+    double bn2 = __hiloint2double(0x7fefffff, -1);
+    if (MN) bn = bn2;
     for (int k = 0; k < kp.ns_pad; k += 2) {
         double g[8];
 #pragma unroll
@@ -350,8 +375,16 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             const double D = fma(h, h, -ca);
             // D finite here.  The ambiguity tests use xor of nested conditions
             // (a implies b: b && !a == a ^ b) so each comparison is issued once.
-            const bool valid = D >= T1;
-            amb = amb || (valid != (D >= nT2));             // -T2 <= D < T1: grazing
+            // MN: one |D| < T1 test (grazing band widened from [-T2, T1) to
+            // (-T1, T1)); D <= -T1 gives a NaN root below, which no comparison
+            // accepts, so `valid` is implied by the candidate test
+            bool valid = true;
+            if (MN) {
+                amb = amb || fabs(D) < T1;
+            } else {
+                valid = D >= T1;
+                amb = amb || (valid != (D >= nT2));         // -T2 <= D < T1: grazing
+            }
             // sa ~ sqrt(D): v_rsq_f64 + one Newton step (sa = t + t*e/2)
             const double r0 = __builtin_amdgcn_rsq(D);
             const double tt = D * r0;
@@ -363,6 +396,16 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             // +0.7 %), elsewhere a select (the fma's constants cost the BVH
             // instantiations registers: sweep -1.4 %)
             const double n = AMGM ? fma(r1 ? -1.0 : 1.0, sa, -h) : (r1 ? n1 : sa - h);
+            if (MN) {
+                // candidates: every chosen root that may reach 1e-4 (n >= thr - M),
+                // straddling ones included -- they are below any sure root, so
+                // the winner's own test after the scan (bn < thrP) catches them
+                const double nt = cand_tag(n, k + e, msk);
+                const double nc = __hiloint2double(n >= thrM ? __double2hiint(nt) : 0x7fefffff, __double2loint(nt));
+                bn2 = dmin_raw(bn2, dmax_raw(bn, nc));
+                bn = dmin_raw(bn, nc);
+                continue;
+            }
             const double tP = CU ? (r1 ? thrP : thrP2) : thrP, tM = CU ? (r1 ? thrM : thrM2) : thrM;
             const bool sure = n >= tP;
             amb = amb || (valid && (sure != (n >= tM)));    // the chosen root straddles 1e-4
@@ -378,7 +421,16 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             if (!RT_CAND_TAG) bk = closer ? k + e : bk;
         }
     }
-    if (RT_CAND_TAG) bk = bn < INF ? (int)((uint32_t)__double2loint(bn) & 0xffffu) : -1;
+    if (MN) {
+        // the winner is sure (its tagged value, within 2^-36 |n| of n, clears
+        // thr + M with that margin) and every other candidate lies more than
+        // 2M above it; no candidate: bn is the sentinel (> 2^1000)
+        const bool any = bn < 0x1p600;
+        amb = amb || (any && (bn < thrP * (1.0 + 0x1p-34) || !(bn2 - bn > M2)));
+        bk = any ? (int)((uint32_t)__double2loint(bn) & 0xffffu) : -1;
+    } else if (RT_CAND_TAG) {
+        bk = bn < INF ? (int)((uint32_t)__double2loint(bn) & 0xffffu) : -1;
+    }
     if (COUNT)
         for (int k = 0; k < kp.ns; ++k) cnt.c[RT_CNT_SPHERE_DISC] += disc_positive(kp.sph[k], o, d, four_a) ? 1 : 0;
     double t = INF;
