@@ -68,9 +68,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #define RT_CAND_TAG 1               // 16 mantissa bits (spheres_closest), so no separate index select
 #endif
 #ifndef RT_CAND_MIN2                // candidate pass: min and second min of the tagged candidates, one
-#define RT_CAND_MIN2 0              // ambiguity test after the scan (A/B knob)
-#endif
-#ifndef RT_AO_FIRST               // AO scenes: the AO direction before the bounce direction (ROLE_AO)
+#define RT_CAND_MIN2 1              // ambiguity test after the scan (r04: C2 +4.3 %; 1: every instantiation but
+#endif                              // CUDA semantics, 2: the sphere-scene queue kernel only)
+#ifndef RT_AO_FIRST                 // AO scenes: the AO direction before the bounce direction (ROLE_AO)
 #define RT_AO_FIRST 1
 #endif
 #ifndef RT_QTASK_TABLE              // sphere-scene queue kernel: tasks decoded per batch into LDS (A/B knob;
@@ -360,7 +360,7 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     // RT_CAND_MIN2: the smallest and second-smallest tagged candidate (bn, bn2;
     // non-candidates enter as a finite sentinel above 2^1000 that keeps the
     // tag), ambiguity decided once after the scan (bn2 - bn <= 2M)
-    constexpr bool MN = RT_CAND_MIN2 && !CU;
+    constexpr bool MN = !CU && (RT_CAND_MIN2 == 1 || (RT_CAND_MIN2 == 2 && AMGM));
     double bn2 = __hiloint2double(0x7fefffff, -1);
     if (MN) bn = bn2;
     for (int k = 0; k < kp.ns_pad; k += 2) {

@@ -16,7 +16,7 @@ if [ -n "$PARITY_LIB" ]; then
   echo "variant parity ($PARITY_LIB): $(tail -1 $O/pytest_variant.log)"
 fi
 if ls tools/variants/*.so >/dev/null 2>&1; then
-  ONLY=${ONLY:-C2,C3} bash tools/ab_configs.sh ${ROUNDS:-2} > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
+  ONLY=${ONLY:-C2,C3,C4} bash tools/ab_configs.sh ${ROUNDS:-2} > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
   cat $O/ab.txt
 fi
 if [ -n "$PCS" ]; then

@@ -24,3 +24,7 @@ import json
 for l in open('$O/cfg_c$c.jsonl'):
     d = json.loads(l); print('cfg chunks', $c, d['config'], d['spp_measured'], d['kernel_msamples_per_s'])"
 done
+for c in ${CHUNKS:-32 16 12 8}; do
+  timeout -k 10 300 python tools/rank_share_rate.py --chunks $c --pipeline --tile-rows 1 > $O/share_c$c.jsonl 2>> $O/share.err || { tail -5 $O/share.err; exit 1; }
+  echo "share chunks $c"; cat $O/share_c$c.jsonl
+done
