@@ -17,10 +17,3 @@ if ls tools/variants/*.so >/dev/null 2>&1; then
   ONLY=${ONLY:-C2,C3,C4,SWEEP} bash tools/ab_configs.sh ${ROUNDS:-2} > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
   cat $O/ab.txt
 fi
-if [ -n "$PCS" ]; then
-cd /tmp
-timeout -k 10 180 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time \
-   --pc-sampling-interval 100 -d $GRAFT_REPO_ROOT/$O/pcs -o pcs --output-format csv \
-   -- python3 $GRAFT_REPO_ROOT/tools/bench_configs.py --only ${PCS} --spp 50 > $GRAFT_REPO_ROOT/$O/pcs.log 2>&1
-echo "pcs rc=$?"; tail -5 $GRAFT_REPO_ROOT/$O/pcs.log; ls -R $GRAFT_REPO_ROOT/$O/pcs | head -20
-fi
