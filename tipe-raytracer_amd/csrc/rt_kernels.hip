@@ -70,6 +70,12 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_CAND_MIN2                // candidate pass: min and second min of the tagged candidates, one
 #define RT_CAND_MIN2 1              // ambiguity test after the scan (r04: C2 +4.3 %; 1: every instantiation but
 #endif                              // CUDA semantics, 2: the sphere-scene queue kernel only)
+#ifndef RT_CAND_GACC                // second-minimum pass: min |D| accumulated, one grazing test per ray (A/B)
+#define RT_CAND_GACC 1              // (r04: C2 +0.3 % over RT_RAW_MIN alone)
+#endif
+#ifndef RT_RAW_MIN                  // normalize's range guard: min of |components| without canonicalizes
+#define RT_RAW_MIN 1
+#endif
 #ifndef RT_AO_FIRST                 // AO scenes: the AO direction before the bounce direction (ROLE_AO)
 #define RT_AO_FIRST 1
 #endif
@@ -121,10 +127,21 @@ __device__ __forceinline__ V3 cross(V3 u, V3 v)
 // normalize(a) = a / sqrt(dot(a, a)), vec3.h:137-139, bit-exact: fast lanes
 // need dot(a,a) in [2^-760, 2^760] and every |component| >= 2^-900 (so zero
 // components, NaN and extreme lengths take the generic path).
+// min(|a|, |b|, |c|) as two v_min_f64 with abs source modifiers: fmin would
+// first canonicalize each operand (one v_max_f64 x, x per component) under
+// IEEE mode.  Only compared against a positive bound; a NaN component makes
+// dot(a, a) NaN, which fails normalize's range test whatever this returns.
+__device__ __forceinline__ double dmin_abs3(double a, double b, double c)
+{
+    double r;
+    asm("v_min_f64 %0, |%1|, |%2|\n\tv_min_f64 %0, %0, |%3|" : "=&v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 __device__ __forceinline__ V3 normalize(V3 a)
 {
     const double n2 = dot(a, a);
-    const double mn = fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
+    const double mn = RT_RAW_MIN ? dmin_abs3(a.x, a.y, a.z) : fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
     if (n2 >= 0x1p-760 && n2 <= 0x1p760 && mn >= 0x1p-900) {
         double L, rc;                    // 1/L from the sqrt sequence's own rsq (rt_device_math.h)
         sqrt_rcp_core(n2, L, rc);
@@ -309,6 +326,14 @@ __device__ __forceinline__ double cand_tag(double n, int k, uint32_t msk)
     return __hiloint2double(__double2hiint(n), (int)lo);
 }
 
+// min(a, |b|) with an abs source modifier (a >= 0; a NaN b drops out, which
+// only happens for a NaN D: non-finite inputs are already ambiguous)
+__device__ __forceinline__ double dmin_abs2(double a, double b)
+{
+    double r;
+    asm("v_min_f64 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 // v_min_f64 / v_max_f64 of two finite, non-NaN operands (the candidate
 // pass's tagged values): fmin/fmax would first canonicalize the bit-built
 // operand (an extra v_max_f64 x, x each).
@@ -323,6 +348,17 @@ __device__ __forceinline__ double dmax_raw(double a, double b)
     double r;
     asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
     return r;
+}
+
+// main.c:214's `r.x > 0.5 || r.y > 0.5 || r.z > 0.5` as max(x, y, z) > 0.5
+// (a NaN component drops out of v_max_f64 exactly as it fails its own
+// comparison; the throughputs are arithmetic results, never signalling
+// NaNs).  The compiler makes the same fold itself, but through fmax, which
+// canonicalizes all three operands first: 6 VALU instead of 3.
+__device__ __forceinline__ bool any_above_half(V3 r)
+{
+    if (!RT_RAW_MIN) return r.x > 0.5 || r.y > 0.5 || r.z > 0.5;
+    return dmax_raw(dmax_raw(r.x, r.y), r.z) > 0.5;
 }
 
 template <bool COUNT, bool CU, bool AMGM = false>
@@ -363,6 +399,7 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     constexpr bool MN = !CU && (RT_CAND_MIN2 == 1 || (RT_CAND_MIN2 == 2 && AMGM));
     double bn2 = __hiloint2double(0x7fefffff, -1);
     if (MN) bn = bn2;
+    double gmin = bn2;                   // (RT_CAND_GACC) min |D| over the scan
     for (int k = 0; k < kp.ns_pad; k += 2) {
         double g[8];
 #pragma unroll
@@ -379,7 +416,9 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             // (-T1, T1)); D <= -T1 gives a NaN root below, which no comparison
             // accepts, so `valid` is implied by the candidate test
             bool valid = true;
-            if (MN) {
+            if (MN && RT_CAND_GACC) {
+                gmin = dmin_abs2(gmin, D);                  // grazing test once, after the scan
+            } else if (MN) {
                 amb = amb || fabs(D) < T1;
             } else {
                 valid = D >= T1;
@@ -426,6 +465,7 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
         // thr + M with that margin) and every other candidate lies more than
         // 2M above it; no candidate: bn is the sentinel (> 2^1000)
         const bool any = bn < 0x1p600;
+        if (RT_CAND_GACC) amb = amb || gmin < T1;
         amb = amb || (any && (bn < thrP * (1.0 + 0x1p-34) || !(bn2 - bn > M2)));
         bk = any ? (int)((uint32_t)__double2loint(bn) & 0xffffu) : -1;
     } else if (RT_CAND_TAG) {
@@ -1300,7 +1340,7 @@ struct LanePath {
                         const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
                         const V3 em = muls(mat.emis, mat.es * 1.5 * AO);
                         inc = inc + mulv(em, r);
-                        if (r.x > 0.5 || r.y > 0.5 || r.z > 0.5) r = mulv(mat.diff, muls(r, 1.3));
+                        if (any_above_half(r)) r = mulv(mat.diff, muls(r, 1.3));
                         rc = mulv(mat.diff, r);
                         // ambient_occlusion's cast (main.c:96-103): from hp along n + random
                         cd = normalize(hn + random_dir<COUNT>(st, cnt));
@@ -1308,7 +1348,7 @@ struct LanePath {
                     } else {
                         const V3 em = muls(mat.emis, mat.es);
                         inc = inc + mulv(em, r);
-                        if (r.x > 0.5 || r.y > 0.5 || r.z > 0.5) r = mulv(mat.diff, muls(r, 1.3));
+                        if (any_above_half(r)) r = mulv(mat.diff, muls(r, 1.3));
                         rc = mulv(mat.diff, r);
                     }
                     if (zero_rc(kp)) {           // black diffuse (a light, a green-then-red wall)
@@ -2435,7 +2475,7 @@ struct QPath {
             const V3 em = muls(emis, es);
             inc = inc + mulv(em, r);
         }
-        if (r.x > 0.5 || r.y > 0.5 || r.z > 0.5) r = mulv(diff, muls(r, 1.3));
+        if (any_above_half(r)) r = mulv(diff, muls(r, 1.3));
         rc = mulv(diff, r);
     }
     __device__ __forceinline__ void shade(const KParams& kp, const Mat& mat) { shade_with(kp, mat.emis, mat.es, mat.diff); }

@@ -12,7 +12,7 @@ for v in ${PARITY_VARIANTS:-c_min2 e_qtail1}; do
      --timeout 300 --timeout-method thread > $O/pytest_$v.log 2>&1 || { tail -30 $O/pytest_$v.log; exit 1; }
   echo "parity $v: $(tail -1 $O/pytest_$v.log)"
 done
-for v in ${SHARE_VARIANTS:-a_base e_qtail1 f_qtail2}; do
+for v in ${SHARE_VARIANTS-a_base e_qtail1 f_qtail2}; do
   for c in ${CHUNKS:-32 12 8}; do
     RT_HIP_LIB=tools/variants/$v.so timeout -k 10 300 python tools/rank_share_rate.py --chunks $c --pipeline --tile-rows 1 > $O/share_${v}_c$c.jsonl 2>> $O/share.err || { tail -5 $O/share.err; exit 1; }
     python3 -c "
