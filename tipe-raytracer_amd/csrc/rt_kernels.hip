@@ -73,6 +73,15 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_CAND_GACC                // second-minimum pass: min |D| accumulated, one grazing test per ray (A/B)
 #define RT_CAND_GACC 1              // (r04: C2 +0.3 % over RT_RAW_MIN alone)
 #endif
+#ifndef RT_QSPHERES                 // sphere-only scenes: a queue-kernel instantiation without triangle code
+#define RT_QSPHERES 1               // (r04: 116 VGPRs, no spills; C2 +2.3 %)
+#endif
+#ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
+#define RT_TRI_BF 1
+#endif
+#ifndef RT_WAVES_PER_SIMD_QS        // occupancy bound of the sphere-only queue kernel (A/B knob)
+#define RT_WAVES_PER_SIMD_QS RT_WAVES_PER_SIMD_Q
+#endif
 #ifndef RT_RAW_MIN                  // normalize's range guard: min of |components| without canonicalizes
 #define RT_RAW_MIN 1
 #endif
@@ -547,6 +556,45 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
     }
 }
 
+// tri_test for the brute-force scan in the caller's order (kp.tri_orig null:
+// no tie rule, `dst < best` is mesh.h's and main.c:82's strict test), with
+// no branches: every lane evaluates det, dst and the barycentrics with the
+// reference operations and one combined condition picks the hit.  The
+// branchy form ran these in nested divergent regions whose exec-mask
+// bookkeeping cost more than the work they skipped: in a wave of
+// incoherent rays some lane almost always passes the culling tests.  Lanes
+// with det < 1e-6 compute a garbage 1/det (the fast reciprocal of a small,
+// zero or negative value) that no condition lets through.
+template <bool CU>
+__device__ __forceinline__ void tri_test_bf(const KParams& kp, int k, const V3 o, const V3 d, double& best, int& kind,
+                                            int& win)
+{
+    const double eps = CU ? 0.00001 : 0.0000001;     // triangle.hu:262 / mesh.h:88
+    const cdptr t = (cdptr)kp.tri + 12 * k;
+    const double ax = t[0], ay = t[1], az = t[2], abx = t[3], aby = t[4], abz = t[5];
+    const double acx = t[6], acy = t[7], acz = t[8], nx = t[9], ny = t[10], nz = t[11];
+    const double det = -(d.x * nx + d.y * ny + d.z * nz);
+    const V3 ao = v3(o.x - ax, o.y - ay, o.z - az);
+    const V3 dao = cross(ao, d);
+    double invDet;
+    if (det <= 0x1p400) invDet = div_core(1.0, det, rcp_refined(det));
+    else invDet = 1 / det;
+    const double dst = (ao.x * nx + ao.y * ny + ao.z * nz) * invDet;
+    const double u = (acx * dao.x + acy * dao.y + acz * dao.z) * invDet;
+    const double v = -(abx * dao.x + aby * dao.y + abz * dao.z) * invDet;
+    const double w = 1 - u - v;
+    // every lane evaluates the whole test: the empty asm keeps the compiler
+    // from sinking the barycentrics under a branch on det and dst
+    double uu = u, vv = v;
+    asm volatile("" : "+v"(uu), "+v"(vv));
+    const bool hit = (det >= 1E-6) & (dst >= eps) & (dst < best) & (uu >= eps) & (vv >= eps) & (w >= eps);
+    if (hit) {
+        best = dst;
+        kind = HIT_TRI;
+        win = k;
+    }
+}
+
 // Triangle BVH traversal (rt_bvh.h: 4-wide nodes collapsed from the binary
 // SAH tree, host build rt_bvh.cpp).  One 128-byte node holds four child
 // boxes (float storage rounded outward; the slab math runs in double); leaf
@@ -863,6 +911,8 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
         // main_cuda.cu:40-45: the ray misses the mesh box, no triangle tested
     } else if (BVH) {
         tris_bvh<COUNT, CU>(kp, o, d, best, kind, win, win_orig, cnt);
+    } else if (RT_TRI_BF && !COUNT && !kp.tri_orig) {
+        for (int k = 0; k < kp.nt; ++k) tri_test_bf<CU>(kp, k, o, d, best, kind, win);
     } else {
         for (int k = 0; k < kp.nt; ++k) tri_test<COUNT, CU, false, true>(kp, k, o, d, best, kind, win, win_orig);
     }
@@ -2315,7 +2365,7 @@ struct QHit {
     bool refr, hole;                 // refraction decided after the direction draws; alpha hole
 };
 
-template <bool SKY, int AOM>
+template <bool SKY, int AOM, bool NT = false>   // NT: the scene has no triangles (every hit is a sphere)
 struct QPath {
     V3 o, d, cd, inc, rc;            // cd: the cast's direction (AO casts; else d)
     double top_n2, best;
@@ -2331,7 +2381,7 @@ struct QPath {
     // the hit, so a refraction lane recomputes it instead of keeping it live).
     __device__ __forceinline__ Mat hit_material(const KParams& kp, V3 hp, V3 hn) const
     {
-        if (kind == HIT_SPHERE) {
+        if (NT || kind == HIT_SPHERE) {
             Mat mat = load_mat(kp.sph_mat + win);
             if (SKY && win == kp.ns - 1) sky_material(kp, win, kp.sph[win], hp, mat);
             return mat;
@@ -2371,7 +2421,7 @@ struct QPath {
                 if (pend) {                              // its direction is still to be made
                     role = ROLE_PBOUNCE;
                     const int pw = pkw & 0x3fffffff;     // the bounce hit's normal (o is its hit point)
-                    if ((pkw >> 30) == HIT_SPHERE) {
+                    if (NT || (pkw >> 30) == HIT_SPHERE) {
                         const SphGeo sg = kp.sph[pw];
                         H.hn = normalize(o - v3(sg.cx, sg.cy, sg.cz));
                     } else {
@@ -2394,7 +2444,7 @@ struct QPath {
             ended = true;
         } else {
             const V3 hp = o + muls(d, best);             // ray_at
-            if (kind == HIT_SPHERE) {
+            if (NT || kind == HIT_SPHERE) {
                 const SphGeo sg = kp.sph[win];
                 H.hn = normalize(hp - v3(sg.cx, sg.cy, sg.cz));
             } else {
@@ -2406,7 +2456,7 @@ struct QPath {
             if (chain) {
                 if (mat.es > 0) {                        // direct view of a light, main.c:154-160
                     V3 col;
-                    if (kind == HIT_SPHERE && !(SKY && win == kp.ns - 1)) {
+                    if ((NT || kind == HIT_SPHERE) && !(SKY && win == kp.ns - 1)) {
                         const double* sd = kp_here()->sph_disp + 3 * win;   // (host: the same round trip)
                         col = v3(sd[0], sd[1], sd[2]);
                     } else {
@@ -2567,7 +2617,8 @@ __device__ __forceinline__ void decode_task(KParamsK K, unsigned t, uint32_t e[k
 }
 
 template <bool SKY, int AOM, int QB>
-__global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(const KParams kp)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QB < 0 ? RT_WAVES_PER_SIMD_QS : RT_WAVES_PER_SIMD_Q)))
+void render_kernel_q(const KParams kp)
 {
     __shared__ double acc_lds[ACC_SLOTS * 256];
     __shared__ uint32_t rng_lds[4 * 256];
@@ -2575,7 +2626,7 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
     uint32_t* rng = rng_lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
     unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
-    QPath<SKY, AOM> L;
+    QPath<SKY, AOM, QB < 0> L;
     L.o = L.d = L.cd = L.inc = L.rc = v3(0, 0, 0);
     L.top_n2 = 1.0;
     L.best = 0.0;
@@ -2652,6 +2703,11 @@ __global__ __launch_bounds__(256, RT_WAVES_PER_SIMD_Q) void render_kernel_q(cons
                 __builtin_amdgcn_s_setprio(0);
 #endif
             }
+        } else if (QB < 0 && L.state == SM_CAST) {          // sphere-only scenes: no triangle scan
+            Cnt cnt;
+            L.win = cast_spheres<false, false, !SKY && AOM != AO_ON>(kp, L.o, L.cast_dir(), L.best, cnt);
+            L.kind = L.win >= 0 ? HIT_SPHERE : HIT_NONE;
+            L.state = SM_RESOLVE;
         } else if (L.state == SM_CAST) {
             Cnt cnt;
             L.kind = closest_hit<false, false, false, !SKY && AOM != AO_ON>(kp, L.o, L.cast_dir(), L.best, L.win, cnt);
@@ -3120,14 +3176,15 @@ static void queue_occupancy_v(bool sky, bool ao, int& nb)
 }
 static unsigned queue_grid(bool sky, bool ao, int qb)
 {
-    static std::atomic<int> cached[12][64];
+    static std::atomic<int> cached[16][64];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? 1 : 2)][dev & 63];
+    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? 1 : qb == 4 ? 2 : 3)][dev & 63];
     int c = slot.load(std::memory_order_relaxed);
     if (c <= 0) {
         int nb = 0, ncu = 0;
-        if (qb == 0) queue_occupancy_v<0>(sky, ao, nb);
+        if (qb == -1) queue_occupancy_v<-1>(sky, ao, nb);
+        else if (qb == 0) queue_occupancy_v<0>(sky, ao, nb);
         else if (qb == 3) queue_occupancy_v<3>(sky, ao, nb);
         else queue_occupancy_v<4>(sky, ao, nb);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -3176,8 +3233,11 @@ int launch_render(const KParams& kp, void* stream)
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
-        if (!qbvh) qb = 0;
-        t_last_kernel = qb == 3 ? "render_kernel_q<QB=3>" : qb == 4 ? "render_kernel_q<QB=4>" : "render_kernel_q<QB=0>";
+        if (!qbvh) qb = RT_QSPHERES && kp.nt == 0 ? -1 : 0;
+        t_last_kernel = qb == 3   ? "render_kernel_q<QB=3>"
+                        : qb == 4 ? "render_kernel_q<QB=4>"
+                        : qb < 0  ? "render_kernel_q<QB=-1>"
+                                  : "render_kernel_q<QB=0>";
         const unsigned nb = queue_grid(sky, ao, qb);
         unsigned long long* tr = nullptr;
         const char* tf = std::getenv("RT_QUEUE_TRACE");
@@ -3194,6 +3254,7 @@ int launch_render(const KParams& kp, void* stream)
                            ? qdiv_magic(kp.chunk_den) : 0u;
         if (qb == 3) queue_launch<3>(sky, ao, nb, st, k2);
         else if (qb == 4) queue_launch<4>(sky, ao, nb, st, k2);
+        else if (qb < 0) queue_launch<-1>(sky, ao, nb, st, k2);
         else queue_launch<0>(sky, ao, nb, st, k2);
         if (tr) {
             std::vector<unsigned long long> h((size_t)nb * 256 * RT_TRACE_WORDS);
