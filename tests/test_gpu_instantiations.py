@@ -1,0 +1,61 @@
+"""Which task-queue instantiation a scene takes, and that each is bit-exact.
+
+r04 splits render_kernel_q by what the scene can reach (DESIGN §4a
+"Instantiations"):
+  * QB = -2: spheres only, every material opaque -- no triangle scan, no
+    alpha-hole or refraction branch compiled in (the C2 bench scene);
+  * QB = -1: spheres only, some material transparent or a hole;
+  * QB = 0: spheres and brute-force triangles (<= 32, no BVH).
+The host picks them (rt_kernels.hip launch_render) from the scene upload's
+material flags.  main.c:196-234 decides per hit: alpha < 0.0001 is a hole,
+alpha <= 0.99 refracts, anything else (NaN included) shades; the opaque
+gate is exactly "no material takes either of the first two branches", so a
+material at alpha = 0.99 must keep the refraction code and one just above
+it must not.  Every render is compared with the oracle bit for bit.
+"""
+import pytest
+
+import helpers
+import tipe_rt
+from tipe_rt import scenes
+
+from test_gpu_bvh_fallback import render_and_compare
+
+pytestmark = pytest.mark.gpu
+
+
+def one_transparent(alpha):
+    """README box plus one extra small sphere of the given alpha in view."""
+    extra = [((0.1, -0.9, -1.8), 0.3, scenes.material((0.8, 0.8, 0.8), alpha=alpha, ior=1.5))]
+    return helpers.SceneBundle(scenes.cornell_spheres(extra=extra))
+
+
+P = dict(W=40, H=30, spp=8, bounces=6)
+
+
+def prm(**kw):
+    q = dict(P)
+    q.update(kw)
+    return helpers.params(q["W"], q["H"], q["spp"], q["bounces"], chunks=4)
+
+
+def test_opaque_sphere_scene_takes_qb_minus2():
+    assert render_and_compare(helpers.cornell(), prm()) == "render_kernel_q<QB=-2>"
+
+
+@pytest.mark.parametrize("alpha", [0.5, 0.99, 0.00005, 0.0])
+def test_transparent_or_hole_sphere_takes_qb_minus1(alpha):
+    assert render_and_compare(one_transparent(alpha), prm()) == "render_kernel_q<QB=-1>"
+
+
+def test_alpha_just_above_refraction_threshold_is_opaque():
+    assert render_and_compare(one_transparent(0.9900001), prm()) == "render_kernel_q<QB=-2>"
+
+
+def test_whole_box_transparent_takes_qb_minus1():
+    bundle = helpers.SceneBundle(scenes.cornell_spheres(alpha=0.5))
+    assert render_and_compare(bundle, prm()) == "render_kernel_q<QB=-1>"
+
+
+def test_triangle_scene_takes_qb0():
+    assert render_and_compare(helpers.pyramid_scene(), prm()) == "render_kernel_q<QB=0>"

@@ -155,6 +155,7 @@ struct rt_device_scene {
     float bvh_rbox = 0.0f;           // >= every |bound| of the BVH's boxes
     bool mats_bounded = false;       // every diffuse/emission/strength finite, |x| <= 2^100
     bool mats_bounded_f32 = false;   // ... |x| <= 2^50: RT_PREC_FP32's em = emis * es * 1.5 * AO stays < FLT_MAX
+    bool sph_opaque = false;         // every sphere material takes main.c's opaque branch (no hole, no refraction)
     double coord_max = HUGE_VAL;     // max |coordinate| of the spheres (|C_a| + R) and triangle vertices
 };
 
@@ -314,6 +315,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.cam_pin = ox == 0.0 && oy == 0.0 && !(p->cam.origin.e[0] == 0.0 && std::signbit(p->cam.origin.e[0])) &&
                  !(p->cam.origin.e[1] == 0.0 && std::signbit(p->cam.origin.e[1])) &&
                  !(p->cam.origin.e[2] == 0.0 && std::signbit(p->cam.origin.e[2]));
+    kp.opaque = sc->sph_opaque ? 1 : 0;
     uni[U_AO] = AO;
     uni[U_WM1] = (double)(p->largeur_image - 1);    // main.c:265 (largeur_image-1)
     uni[U_HM1] = (double)(p->hauteur_image - 1);
@@ -816,6 +818,8 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->device = device;
     ds->mats_bounded = mats_bounded;
     ds->mats_bounded_f32 = mats_bounded_f32;
+    ds->sph_opaque = std::all_of(sph_mat.begin(), sph_mat.end(),
+                                 [](const DevMat& m) { return !(m.alpha < 0.0001) && !(m.alpha <= 0.99); });
     ds->coord_max = coord_max;
     ds->ns = scene->nbSpheres;
     ds->ns_pad = ns_pad;

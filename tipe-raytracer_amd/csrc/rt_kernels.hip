@@ -76,6 +76,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_QSPHERES                 // sphere-only scenes: a queue-kernel instantiation without triangle code
 #define RT_QSPHERES 1               // (r04: 116 VGPRs, no spills; C2 +2.3 %)
 #endif
+#ifndef RT_QOPAQUE                  // sphere-only scenes whose materials are all opaque: an instantiation without
+#define RT_QOPAQUE 1                // the alpha-hole and refraction code (r04: 109 VGPRs; C2 +1.0 %)
+#endif
 #ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
 #define RT_TRI_BF 1
 #endif
@@ -2365,7 +2368,10 @@ struct QHit {
     bool refr, hole;                 // refraction decided after the direction draws; alpha hole
 };
 
-template <bool SKY, int AOM, bool NT = false>   // NT: the scene has no triangles (every hit is a sphere)
+// NT: the scene has no triangles (every hit is a sphere); OP: every material
+// is opaque (host: !(alpha < 0.0001) && !(alpha <= 0.99), so no alpha hole
+// and no refraction branch is ever taken and neither is compiled in)
+template <bool SKY, int AOM, bool NT = false, bool OP = false>
 struct QPath {
     V3 o, d, cd, inc, rc;            // cd: the cast's direction (AO casts; else d)
     double top_n2, best;
@@ -2466,10 +2472,10 @@ struct QPath {
                     acc_add(acc, ACC_ALB, col);
                     acc_add(acc, ACC_NRM, H.hn);
                     lit = true;
-                } else if (!(mat.alpha < 0.0001) || i == kp.B - 1) {
+                } else if (OP || !(mat.alpha < 0.0001) || i == kp.B - 1) {
                     acc_add(acc, ACC_ALB, mat.diff);
                     acc_add(acc, ACC_NRM, H.hn);
-                    chain = mat.alpha < 0.0001;
+                    chain = !OP && mat.alpha < 0.0001;
                 }
             }
             if (lit) {
@@ -2479,13 +2485,13 @@ struct QPath {
                 o = hp;
                 H.rs = mat.rs;
                 H.refr = false;
-                H.hole = mat.alpha < 0.0001;
+                H.hole = !OP && mat.alpha < 0.0001;
                 if (H.hole) {                              // alpha H.hole: straight on, main.c:200-206;
                     if (i + 1 >= kp.B) ended = true;     // its direction draws are made (and unused)
                     else role = ROLE_BOUNCE;             // so the stream's block cache stays in order
                 } else {
                     chain = false;
-                    if (mat.alpha <= 0.99) {             // refraction: decided after the direction draws
+                    if (!OP && mat.alpha <= 0.99) {      // refraction: decided after the direction draws
                         H.refr = true;
                         role = ROLE_BOUNCE;
                     } else {
@@ -2533,7 +2539,7 @@ struct QPath {
     // After next_ray gave a bounce lane its diffuse direction dn.
     __device__ __forceinline__ void finish_bounce(const KParams& kp, V3 dn, Stream& st, double* acc, const QHit& H)
     {
-        if (H.hole) {                                      // the ray goes on unchanged from the hit point
+        if (!OP && H.hole) {                               // the ray goes on unchanged from the hit point
             ++i;
             cd = d;
             state = SM_CAST;
@@ -2542,7 +2548,7 @@ struct QPath {
         const V3 reflected_dir = d - muls(H.hn, 2 * dot(d, H.hn));
         const V3 dr = dn + muls(reflected_dir - dn, H.rs);
         bool shaded = true;
-        if (H.refr) {                                      // main.c:167-193
+        if (!OP && H.refr) {                               // main.c:167-193
             const Mat mat = hit_material(kp, o, H.hn);
             V3 nn = H.hn;
             double n1, n2;
@@ -2568,7 +2574,7 @@ struct QPath {
             d = dr;
         }
         bool ended = false;
-        if (H.refr && shaded) ended = zero_rc(kp);
+        if (!OP && H.refr && shaded) ended = zero_rc(kp);
         if (AOM == AO_ON && shaded && !ended && i + 1 < kp.B) {
             // ambient_occlusion's cast (main.c:96-103): from the hit along n + random
             Cnt cnt;
@@ -2626,7 +2632,7 @@ void render_kernel_q(const KParams kp)
     uint32_t* rng = rng_lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
     unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
-    QPath<SKY, AOM, QB < 0> L;
+    QPath<SKY, AOM, QB < 0, QB == -2> L;
     L.o = L.d = L.cd = L.inc = L.rc = v3(0, 0, 0);
     L.top_n2 = 1.0;
     L.best = 0.0;
@@ -3176,14 +3182,15 @@ static void queue_occupancy_v(bool sky, bool ao, int& nb)
 }
 static unsigned queue_grid(bool sky, bool ao, int qb)
 {
-    static std::atomic<int> cached[16][64];
+    static std::atomic<int> cached[20][64];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? 1 : qb == 4 ? 2 : 3)][dev & 63];
+    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? 1 : qb == 4 ? 2 : qb == -1 ? 3 : 4)][dev & 63];
     int c = slot.load(std::memory_order_relaxed);
     if (c <= 0) {
         int nb = 0, ncu = 0;
-        if (qb == -1) queue_occupancy_v<-1>(sky, ao, nb);
+        if (qb == -2) queue_occupancy_v<-2>(sky, ao, nb);
+        else if (qb == -1) queue_occupancy_v<-1>(sky, ao, nb);
         else if (qb == 0) queue_occupancy_v<0>(sky, ao, nb);
         else if (qb == 3) queue_occupancy_v<3>(sky, ao, nb);
         else queue_occupancy_v<4>(sky, ao, nb);
@@ -3233,9 +3240,10 @@ int launch_render(const KParams& kp, void* stream)
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
-        if (!qbvh) qb = RT_QSPHERES && kp.nt == 0 ? -1 : 0;
+        if (!qbvh) qb = RT_QSPHERES && kp.nt == 0 ? (RT_QOPAQUE && kp.opaque ? -2 : -1) : 0;
         t_last_kernel = qb == 3   ? "render_kernel_q<QB=3>"
                         : qb == 4 ? "render_kernel_q<QB=4>"
+                        : qb == -2 ? "render_kernel_q<QB=-2>"
                         : qb < 0  ? "render_kernel_q<QB=-1>"
                                   : "render_kernel_q<QB=0>";
         const unsigned nb = queue_grid(sky, ao, qb);
@@ -3254,6 +3262,7 @@ int launch_render(const KParams& kp, void* stream)
                            ? qdiv_magic(kp.chunk_den) : 0u;
         if (qb == 3) queue_launch<3>(sky, ao, nb, st, k2);
         else if (qb == 4) queue_launch<4>(sky, ao, nb, st, k2);
+        else if (qb == -2) queue_launch<-2>(sky, ao, nb, st, k2);
         else if (qb < 0) queue_launch<-1>(sky, ao, nb, st, k2);
         else queue_launch<0>(sky, ao, nb, st, k2);
         if (tr) {
