@@ -100,8 +100,6 @@ struct KParams {
     int useAO;
     int zero_exit;           // paths end once rayColor == 0 (host: only where exact, LanePath::zero_rc)
     int cam_pin;             // aperture 0 and no -0 camera coordinate: co + (jx*0, jy*0, 0) == co exactly
-    int opaque;              // every sphere material opaque: !(alpha < 0.0001) && !(alpha <= 0.99) (no hole,
-                             // no refraction; the queue kernel's QB = -2 instantiation)
     uint32_t key0, key1;
     int chunks;              // samples of a pixel split into this many chunks
     int chunk_taper;         // rt_chunk_bound's taper levels L (0: equal slices)
@@ -124,6 +122,9 @@ struct KParams {
                                                  // chunks (udiv_q); qm_chunks 0: 64-bit chunk starts
     unsigned long long* trace;   // render_kernel_q diagnostics (RT_QUEUE_TRACE), normally null
     unsigned long long* counters;
+    int opaque;              // every sphere material opaque: !(alpha < 0.0001) && !(alpha <= 0.99) (no hole,
+                             // no refraction; the queue kernel's QB = -2 instantiation).  Last, so the
+                             // other fields keep their kernarg offsets (and the kernels their SMEM loads)
 };
 
 struct UniBlock { double v[U_COUNT]; };
