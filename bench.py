@@ -687,7 +687,7 @@ def main():
                          "traffic_model_note": "model: render kernel = chunks x px x 72 B partial writes; frame = "
                                                "that x 2 (combine_kernel reads them) + 72 B/px output; `traffic` "
                                                "is the last committed rocprofv3 PMC value (traffic_source)",
-                         "kernel": "render_kernel_q<false, 0, -2> (persistent task queue, sphere-only opaque-material instantiation; no sky, no AO, no BVH) + combine_kernel",
+                         "kernel": "render_kernel_q<false, 0, -2, false> (persistent task queue, sphere-only opaque-material instantiation; no sky, no AO, no BVH) + combine_kernel",
                          "kernel_ms": round(kernel_ms, 3), "flops_per_launch": flops,
                          "flops_per_sample": round(flops / launch_samples, 1),
                          "note": "achieved = algorithmic FLOPs of the work done (SURVEY 8d formula on the "

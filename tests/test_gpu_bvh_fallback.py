@@ -65,9 +65,10 @@ def test_deep_tree_without_binary16_nodes_takes_fixed_grid():
 
 def test_deep_tree_with_binary16_nodes_takes_queue_qb3():
     """Control: the same tree without the far triangle packs, and runs the
-    deep-tree queue kernel."""
+    deep-tree queue kernel (its opaque-material instantiation: the tree's
+    texels and the README spheres are opaque, test_gpu_instantiations.py)."""
     p = helpers.params(40, 30, 6, 8, use_ao=True, chunks=4)
-    assert render_and_compare(helpers.tree_scene(), p) == "render_kernel_q<QB=3>"
+    assert render_and_compare(helpers.tree_scene(), p) == "render_kernel_q<QB=3,OP>"
 
 
 def test_shallow_tree_without_binary16_nodes_keeps_queue_qb4():

@@ -5,7 +5,10 @@ r04 splits render_kernel_q by what the scene can reach (DESIGN §4a
   * QB = -2: spheres only, every material opaque -- no triangle scan, no
     alpha-hole or refraction branch compiled in (the C2 bench scene);
   * QB = -1: spheres only, some material transparent or a hole;
-  * QB = 0: spheres and brute-force triangles (<= 32, no BVH).
+  * QB = 0: spheres and brute-force triangles (<= 32, no BVH);
+  * QB = 3 with OPQ: the deep-tree kernel when every sphere material, every
+    texel and every material index (no 3 or 4, tri_material's overrides)
+    is opaque (C4).
 The host picks them (rt_kernels.hip launch_render) from the scene upload's
 material flags.  main.c:196-234 decides per hit: alpha < 0.0001 is a hole,
 alpha <= 0.99 refracts, anything else (NaN included) shades; the opaque
@@ -59,3 +62,36 @@ def test_whole_box_transparent_takes_qb_minus1():
 
 def test_triangle_scene_takes_qb0():
     assert render_and_compare(helpers.pyramid_scene(), prm()) == "render_kernel_q<QB=0>"
+
+
+def test_tree_scene_takes_deep_tree_opaque_instantiation():
+    """C4: README spheres + the 1320-triangle tree, all opaque."""
+    p = helpers.params(40, 30, 6, 8, use_ao=True, chunks=4)
+    assert render_and_compare(helpers.tree_scene(), p) == "render_kernel_q<QB=3,OP>"
+
+
+def test_tree_scene_with_transparent_sphere_keeps_qb3():
+    extra = [((0.1, -0.9, -1.8), 0.3, scenes.material((0.8, 0.8, 0.8), alpha=0.5, ior=1.5))]
+    bundle = helpers.SceneBundle(scenes.cornell_spheres(extra=extra),
+                                 scenes.moved(scenes.load_tree_fixture(), scenes.TREE_MOVE))
+    p = helpers.params(40, 30, 6, 8, use_ao=True, chunks=4)
+    assert render_and_compare(bundle, p) == "render_kernel_q<QB=3>"
+
+
+@pytest.mark.parametrize("mat_index", [3, 4])
+def test_tree_with_override_material_keeps_qb3(mat_index):
+    """tri_material's material indices 3 and 4 force alpha 0.1 / 0.6 whatever
+    the texel holds: a tree whose first triangles use one of them is not
+    opaque.  The texel table gets entries up to that index (copies of
+    material 0), so the scene stays valid."""
+    tris, qm, mats, tw, th, nm = scenes.moved(scenes.load_tree_fixture(), scenes.TREE_MOVE)
+    from tipe_rt.types import Material
+    n_new = max(nm, mat_index + 1)
+    mats2 = (Material * (n_new * tw * th))()
+    for k in range(n_new * tw * th):
+        mats2[k] = mats[k] if k < nm * tw * th else mats[0]
+    for k in range(0, len(tris), 7):
+        qm[k] = mat_index
+    bundle = helpers.SceneBundle(scenes.cornell_spheres(), (tris, qm, mats2, tw, th, n_new))
+    p = helpers.params(40, 30, 6, 8, use_ao=True, chunks=4)
+    assert render_and_compare(bundle, p) == "render_kernel_q<QB=3>"

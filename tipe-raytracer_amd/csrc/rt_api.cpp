@@ -156,6 +156,7 @@ struct rt_device_scene {
     bool mats_bounded = false;       // every diffuse/emission/strength finite, |x| <= 2^100
     bool mats_bounded_f32 = false;   // ... |x| <= 2^50: RT_PREC_FP32's em = emis * es * 1.5 * AO stays < FLT_MAX
     bool sph_opaque = false;         // every sphere material takes main.c's opaque branch (no hole, no refraction)
+    bool tri_opaque = false;         // ... every texel too, and no triangle uses material index 3 or 4
     double coord_max = HUGE_VAL;     // max |coordinate| of the spheres (|C_a| + R) and triangle vertices
 };
 
@@ -316,6 +317,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
                  !(p->cam.origin.e[1] == 0.0 && std::signbit(p->cam.origin.e[1])) &&
                  !(p->cam.origin.e[2] == 0.0 && std::signbit(p->cam.origin.e[2]));
     kp.opaque = sc->sph_opaque ? 1 : 0;
+    kp.opaque_all = sc->sph_opaque && (sc->nt == 0 || sc->tri_opaque) ? 1 : 0;
     uni[U_AO] = AO;
     uni[U_WM1] = (double)(p->largeur_image - 1);    // main.c:265 (largeur_image-1)
     uni[U_HM1] = (double)(p->hauteur_image - 1);
@@ -818,8 +820,14 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->device = device;
     ds->mats_bounded = mats_bounded;
     ds->mats_bounded_f32 = mats_bounded_f32;
-    ds->sph_opaque = std::all_of(sph_mat.begin(), sph_mat.end(),
-                                 [](const DevMat& m) { return !(m.alpha < 0.0001) && !(m.alpha <= 0.99); });
+    const auto opaque_mat = [](const DevMat& m) { return !(m.alpha < 0.0001) && !(m.alpha <= 0.99); };
+    ds->sph_opaque = std::all_of(sph_mat.begin(), sph_mat.end(), opaque_mat);
+    // tri_material (rt_kernels.hip): the texel's alpha, overridden for
+    // material indices 1 (1.0), 3 (0.1) and 4 (0.6); the texel index is
+    // clamped into the whole table, so every texel counts
+    ds->tri_opaque = std::all_of(texels.begin(), texels.end(), opaque_mat);
+    for (int i = 0; i < scene->nbTriangles && ds->tri_opaque; ++i)
+        if (scene->quelMatPourTri[i] == 3 || scene->quelMatPourTri[i] == 4) ds->tri_opaque = false;
     ds->coord_max = coord_max;
     ds->ns = scene->nbSpheres;
     ds->ns_pad = ns_pad;

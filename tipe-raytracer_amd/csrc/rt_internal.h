@@ -125,6 +125,8 @@ struct KParams {
     int opaque;              // every sphere material opaque: !(alpha < 0.0001) && !(alpha <= 0.99) (no hole,
                              // no refraction; the queue kernel's QB = -2 instantiation).  Last, so the
                              // other fields keep their kernarg offsets (and the kernels their SMEM loads)
+    int opaque_all;          // ... and so is every triangle material: every texel, no material index 3 or 4
+                             // (tri_material's alpha overrides); the deep-tree OPQ instantiation
 };
 
 struct UniBlock { double v[U_COUNT]; };

@@ -79,6 +79,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_QOPAQUE                  // sphere-only scenes whose materials are all opaque: an instantiation without
 #define RT_QOPAQUE 1                // the alpha-hole and refraction code (r04: 109 VGPRs; C2 +1.0 %)
 #endif
+#ifndef RT_QOPAQUE_BVH              // deep-tree queue kernel for scenes whose every material (spheres, texels,
+#define RT_QOPAQUE_BVH 1            // no material index 3 / 4) is opaque: no hole / refraction code (r04: C4 +2.9 %)
+#endif
 #ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
 #define RT_TRI_BF 1
 #endif
@@ -2622,7 +2625,7 @@ __device__ __forceinline__ void decode_task(KParamsK K, unsigned t, uint32_t e[k
     e[4] = (uint32_t)chunk_start(K->S, K->chunks, K->chunk_taper, K->chunk_den, K->qm_chunks, chunk + 1u);
 }
 
-template <bool SKY, int AOM, int QB>
+template <bool SKY, int AOM, int QB, bool OPQ = false>   // OPQ: (BVH scenes) every material opaque
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QB < 0 ? RT_WAVES_PER_SIMD_QS : RT_WAVES_PER_SIMD_Q)))
 void render_kernel_q(const KParams kp)
 {
@@ -2632,7 +2635,7 @@ void render_kernel_q(const KParams kp)
     uint32_t* rng = rng_lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
     unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
-    QPath<SKY, AOM, QB < 0, QB == -2> L;
+    QPath<SKY, AOM, QB < 0, QB == -2 || OPQ> L;
     L.o = L.d = L.cd = L.inc = L.rc = v3(0, 0, 0);
     L.top_n2 = 1.0;
     L.best = 0.0;
@@ -3162,36 +3165,37 @@ static void launch_variant(const KParams& kp_in, void* stream)
 }
 
 #if RT_QUEUE > 0
-template <bool SKY, int AOM, int QB>
+template <bool SKY, int AOM, int QB, bool OPQ = false>
 static void queue_occupancy(int& nb)
 {
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<SKY, AOM, QB>, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, render_kernel_q<SKY, AOM, QB, OPQ>, 256, 0);
 }
 
 // Resident blocks of the queue kernel on this device (grid of render_kernel_q).
 // Cached per device and variant; rt_fill_canva may run on several host
 // threads at once (main.c's pthreads), so the cache is atomic (every thread
 // computes the same value).
-template <int QB>
+template <int QB, bool OPQ = false>
 static void queue_occupancy_v(bool sky, bool ao, int& nb)
 {
-    if (sky && ao) queue_occupancy<true, AO_ON, QB>(nb);
-    else if (sky) queue_occupancy<true, AO_OFF, QB>(nb);
-    else if (ao) queue_occupancy<false, AO_ON, QB>(nb);
-    else queue_occupancy<false, AO_OFF, QB>(nb);
+    if (sky && ao) queue_occupancy<true, AO_ON, QB, OPQ>(nb);
+    else if (sky) queue_occupancy<true, AO_OFF, QB, OPQ>(nb);
+    else if (ao) queue_occupancy<false, AO_ON, QB, OPQ>(nb);
+    else queue_occupancy<false, AO_OFF, QB, OPQ>(nb);
 }
-static unsigned queue_grid(bool sky, bool ao, int qb)
+static unsigned queue_grid(bool sky, bool ao, int qb, bool opq)
 {
-    static std::atomic<int> cached[20][64];
+    static std::atomic<int> cached[24][64];
     int dev = 0;
     (void)hipGetDevice(&dev);
-    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? 1 : qb == 4 ? 2 : qb == -1 ? 3 : 4)][dev & 63];
+    std::atomic<int>& slot = cached[(sky ? 1 : 0) + (ao ? 2 : 0) + 4 * (qb == 0 ? 0 : qb == 3 ? (opq ? 5 : 1) : qb == 4 ? 2 : qb == -1 ? 3 : 4)][dev & 63];
     int c = slot.load(std::memory_order_relaxed);
     if (c <= 0) {
         int nb = 0, ncu = 0;
         if (qb == -2) queue_occupancy_v<-2>(sky, ao, nb);
         else if (qb == -1) queue_occupancy_v<-1>(sky, ao, nb);
         else if (qb == 0) queue_occupancy_v<0>(sky, ao, nb);
+        else if (qb == 3 && opq) queue_occupancy_v<3, true>(sky, ao, nb);
         else if (qb == 3) queue_occupancy_v<3>(sky, ao, nb);
         else queue_occupancy_v<4>(sky, ao, nb);
         (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -3205,13 +3209,13 @@ static unsigned queue_grid(bool sky, bool ao, int qb)
     return (unsigned)c;
 }
 
-template <int QB>
+template <int QB, bool OPQ = false>
 static void queue_launch(bool sky, bool ao, unsigned nb, hipStream_t st, const KParams& k2)
 {
-    if (sky && ao) hipLaunchKernelGGL((render_kernel_q<true, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
-    else if (sky) hipLaunchKernelGGL((render_kernel_q<true, AO_OFF, QB>), dim3(nb), dim3(256), 0, st, k2);
-    else if (ao) hipLaunchKernelGGL((render_kernel_q<false, AO_ON, QB>), dim3(nb), dim3(256), 0, st, k2);
-    else hipLaunchKernelGGL((render_kernel_q<false, AO_OFF, QB>), dim3(nb), dim3(256), 0, st, k2);
+    if (sky && ao) hipLaunchKernelGGL((render_kernel_q<true, AO_ON, QB, OPQ>), dim3(nb), dim3(256), 0, st, k2);
+    else if (sky) hipLaunchKernelGGL((render_kernel_q<true, AO_OFF, QB, OPQ>), dim3(nb), dim3(256), 0, st, k2);
+    else if (ao) hipLaunchKernelGGL((render_kernel_q<false, AO_ON, QB, OPQ>), dim3(nb), dim3(256), 0, st, k2);
+    else hipLaunchKernelGGL((render_kernel_q<false, AO_OFF, QB, OPQ>), dim3(nb), dim3(256), 0, st, k2);
 }
 
 // floor((2^32 - 1) / d) for udiv_q
@@ -3241,12 +3245,13 @@ int launch_render(const KParams& kp, void* stream)
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
         if (!qbvh) qb = RT_QSPHERES && kp.nt == 0 ? (RT_QOPAQUE && kp.opaque ? -2 : -1) : 0;
-        t_last_kernel = qb == 3   ? "render_kernel_q<QB=3>"
+        const bool opq = RT_QOPAQUE_BVH && qb == 3 && kp.opaque_all;
+        t_last_kernel = qb == 3   ? (opq ? "render_kernel_q<QB=3,OP>" : "render_kernel_q<QB=3>")
                         : qb == 4 ? "render_kernel_q<QB=4>"
                         : qb == -2 ? "render_kernel_q<QB=-2>"
                         : qb < 0  ? "render_kernel_q<QB=-1>"
                                   : "render_kernel_q<QB=0>";
-        const unsigned nb = queue_grid(sky, ao, qb);
+        const unsigned nb = queue_grid(sky, ao, qb, opq);
         unsigned long long* tr = nullptr;
         const char* tf = std::getenv("RT_QUEUE_TRACE");
         if (tf) (void)hipMalloc((void**)&tr, (size_t)nb * 256 * RT_TRACE_WORDS * sizeof(unsigned long long));
@@ -3260,7 +3265,8 @@ int launch_render(const KParams& kp, void* stream)
         // chunk starts c*S/P in 32 bits when (P + 1) * S fits
         k2.qm_chunks = (unsigned long long)(kp.chunk_den + 1) * (unsigned long long)kp.S < (1ull << 32)
                            ? qdiv_magic(kp.chunk_den) : 0u;
-        if (qb == 3) queue_launch<3>(sky, ao, nb, st, k2);
+        if (qb == 3 && opq) queue_launch<3, true>(sky, ao, nb, st, k2);
+        else if (qb == 3) queue_launch<3>(sky, ao, nb, st, k2);
         else if (qb == 4) queue_launch<4>(sky, ao, nb, st, k2);
         else if (qb == -2) queue_launch<-2>(sky, ao, nb, st, k2);
         else if (qb < 0) queue_launch<-1>(sky, ao, nb, st, k2);

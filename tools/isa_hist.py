@@ -21,7 +21,7 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SYM = sys.argv[1] if len(sys.argv) > 1 else "_ZN2rt15render_kernel_qILb0ELi0ELin2EEEvNS_7KParamsE"
+SYM = sys.argv[1] if len(sys.argv) > 1 else "_ZN2rt15render_kernel_qILb0ELi0ELin2ELb0EEEvNS_7KParamsE"
 ASM = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "tipe-raytracer_amd", "rt_kernels_g.s")
 SRC = {"rt_kernels.hip": os.path.join(ROOT, "tipe-raytracer_amd", "csrc", "rt_kernels.hip"),
        "rt_device_math.h": os.path.join(ROOT, "tipe-raytracer_amd", "csrc", "rt_device_math.h")}

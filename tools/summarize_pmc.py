@@ -10,7 +10,7 @@ os.makedirs(dst, exist_ok=True)
 def rows(d):
     p = os.path.join(src, d, "run_counter_collection.csv")
     return list(csv.DictReader(open(p))) if os.path.exists(p) else []
-KNAME = os.environ.get("KNAME", "render_kernel_q<false, 0, -2>")     # the C2 hot kernel (r03: <false, 0, 0>; r01: render_kernel<false, false, false>)
+KNAME = os.environ.get("KNAME", "render_kernel_q<false, 0, -2, false>")     # the C2 hot kernel (r03: <false, 0, 0>; r01: render_kernel<false, false, false>)
 def per_dispatch(d, counter, kname=KNAME):
     acc = {}
     for r in rows(d):
