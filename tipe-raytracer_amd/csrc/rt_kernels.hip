@@ -82,6 +82,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_QOPAQUE_BVH              // deep-tree queue kernel for scenes whose every material (spheres, texels,
 #define RT_QOPAQUE_BVH 1            // no material index 3 / 4) is opaque: no hole / refraction code (r04: C4 +2.9 %)
 #endif
+#ifndef RT_QPIN                     // the QB = -2 instantiation also requires a pinned camera (A/B knob)
+#define RT_QPIN 0                   // (r04: no VGPR change, 109 either way; not measured)
+#endif
 #ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
 #define RT_TRI_BF 1
 #endif
@@ -2906,7 +2909,7 @@ void render_kernel_q(const KParams kp)
                 const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
                 const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));     // get_ray, camera.h:42-55
                 const V3 dest = co + muls(dir, U[b + U_FOCUS]);
-                if (kp.cam_pin) {                              // zero aperture: the origin itself (host-checked)
+                if ((RT_QPIN && QB == -2) || kp.cam_pin) {     // zero aperture: the origin itself (host-checked)
                     no = co;
                 } else {
                     const double jx = -0.5 + 1.0 * unit31(w.next31());
@@ -3244,7 +3247,7 @@ int launch_render(const KParams& kp, void* stream)
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
-        if (!qbvh) qb = RT_QSPHERES && kp.nt == 0 ? (RT_QOPAQUE && kp.opaque ? -2 : -1) : 0;
+        if (!qbvh) qb = RT_QSPHERES && kp.nt == 0 ? (RT_QOPAQUE && kp.opaque && (!RT_QPIN || kp.cam_pin) ? -2 : -1) : 0;
         const bool opq = RT_QOPAQUE_BVH && qb == 3 && kp.opaque_all;
         t_last_kernel = qb == 3   ? (opq ? "render_kernel_q<QB=3,OP>" : "render_kernel_q<QB=3>")
                         : qb == 4 ? "render_kernel_q<QB=4>"
