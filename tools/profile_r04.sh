@@ -20,7 +20,7 @@ step bench
 timeout -k 10 400 python3 bench.py --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cut -c1-400 $OUT/bench.json; echo
 step kernel-trace
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras > $OUT/kt.log 2>&1 || { tail -20 $OUT/kt.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras --no-pipeline > $OUT/kt.log 2>&1 || { tail -20 $OUT/kt.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt_cfg -o run --output-format csv -- python3 tools/bench_configs.py > $OUT/kt_cfg.log 2>&1 || { tail -20 $OUT/kt_cfg.log; exit 1; }
 step pmc
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-format csv -- $B > $OUT/fetch.log 2>&1 || { tail -5 $OUT/fetch.log; exit 1; }
