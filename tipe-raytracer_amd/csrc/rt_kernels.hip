@@ -85,6 +85,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_QPIN                     // the QB = -2 instantiation also requires a pinned camera (A/B knob)
 #define RT_QPIN 0                   // (r04: no VGPR change, 109 either way; not measured)
 #endif
+#ifndef RT_BOX_MM                   // slab test as one comparison max(tmin, -sabs) <= min(tmax, cull) (A/B knob)
+#define RT_BOX_MM 0
+#endif
 #ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
 #define RT_TRI_BF 1
 #endif
@@ -736,7 +739,8 @@ __device__ __forceinline__ void box4(const KParams& kp, const BvhNode4* nd, cons
     for (int c = 0; c < 4; ++c) {
         const float tmin = fmaxf(fmaxf(fmaf(Px[c], r.ix, r.ax), fmaf(Py[c], r.iy, r.ay)), fmaf(Pz[c], r.iz, r.az));
         const float tmax = fminf(fminf(fmaf(Qx[c], r.ix, r.bx), fmaf(Qy[c], r.iy, r.by)), fmaf(Qz[c], r.iz, r.bz));
-        h[c] = Cn[c] >= 0 && tmin <= tmax && tmax >= nsabs && tmin <= cull;
+        h[c] = Cn[c] >= 0 && (RT_BOX_MM ? fmaxf(tmin, nsabs) <= fminf(tmax, cull)
+                                        : tmin <= tmax && tmax >= nsabs && tmin <= cull);
         tn[c] = tmin;
     }
 }
@@ -784,7 +788,10 @@ __device__ __forceinline__ void box4h(const KParams& kp, const BvhNodeH* nd, uin
         Cn[c] = nib == 15 ? -1 : nib;
         const float tmin = fmaxf(fmaxf(fmaf(Px[c], r.ix, Ax), fmaf(Py[c], r.iy, Ay)), fmaf(Pz[c], r.iz, Az));
         const float tmax = fminf(fminf(fmaf(Qx[c], r.ix, Bx), fmaf(Qy[c], r.iy, By)), fmaf(Qz[c], r.iz, Bz));
-        h[c] = nib != 15 && tmin <= tmax && tmax >= nsabs && tmin <= cull;
+        // RT_BOX_MM: max(tmin, -sabs) <= min(tmax, cull) is the same three
+        // tests (-sabs < 0 <= cull) with one comparison instead of three
+        h[c] = nib != 15 && (RT_BOX_MM ? fmaxf(tmin, nsabs) <= fminf(tmax, cull)
+                                       : tmin <= tmax && tmax >= nsabs && tmin <= cull);
         tn[c] = tmin;
     }
 }
@@ -2468,7 +2475,8 @@ struct QPath {
             if (chain) {
                 if (mat.es > 0) {                        // direct view of a light, main.c:154-160
                     V3 col;
-                    if ((NT || kind == HIT_SPHERE) && !(SKY && win == kp.ns - 1)) {
+                    // (OP: no triangle emits -- the host's gate -- so a lit hit is a sphere)
+                    if ((NT || (RT_OPQ_NOEMIT && OP) || kind == HIT_SPHERE) && !(SKY && win == kp.ns - 1)) {
                         const double* sd = kp_here()->sph_disp + 3 * win;   // (host: the same round trip)
                         col = v3(sd[0], sd[1], sd[2]);
                     } else {
