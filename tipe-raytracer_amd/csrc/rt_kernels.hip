@@ -88,6 +88,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_BOX_MM                   // slab test as one comparison max(tmin, -sabs) <= min(tmax, cull) (A/B knob)
 #define RT_BOX_MM 0
 #endif
+#ifndef RT_LEAF_BF                  // BVH leaf triangle test without nested branches (A/B knob)
+#define RT_LEAF_BF 0
+#endif
 #ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
 #define RT_TRI_BF 1
 #endif
@@ -543,6 +546,30 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
         g = kp.tri[k];
     }
     const double det = -(d.x * g.nx + d.y * g.ny + d.z * g.nz);
+    if (RT_LEAF_BF && O32) {
+        // the BVH leaf test without nested branches (RT_LEAF_BF): every lane
+        // evaluates the reference's operations; the tie rule reads the
+        // caller's index unconditionally
+        const V3 ao = v3(o.x - g.ax, o.y - g.ay, o.z - g.az);
+        const V3 dao = cross(ao, d);
+        double invDet;
+        if (det <= 0x1p400) invDet = div_core(1.0, det, rcp_refined(det));
+        else invDet = 1 / det;
+        const double dst = (ao.x * g.nx + ao.y * g.ny + ao.z * g.nz) * invDet;
+        double u = (g.acx * dao.x + g.acy * dao.y + g.acz * dao.z) * invDet;
+        double v = -(g.abx * dao.x + g.aby * dao.y + g.abz * dao.z) * invDet;
+        asm volatile("" : "+v"(u), "+v"(v));
+        const double w = 1 - u - v;
+        const int orig = !kp.tri_orig ? k : *(const int*)((const char*)kp.tri_orig + (uint32_t)k * 4u);
+        const bool closer = (dst < best) | ((dst == best) & (kind == HIT_TRI) & (orig < win_orig));
+        if ((det >= 1E-6) & (dst >= eps) & closer & (u >= eps) & (v >= eps) & (w >= eps)) {
+            best = dst;
+            kind = HIT_TRI;
+            win = k;
+            win_orig = orig;
+        }
+        return;
+    }
     if (det >= 1E-6) {
         const V3 ao = v3(o.x - g.ax, o.y - g.ay, o.z - g.az);
         const V3 dao = cross(ao, d);
