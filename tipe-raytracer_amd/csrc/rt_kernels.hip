@@ -86,7 +86,7 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #define RT_QPIN 0                   // (r04: no VGPR change, 109 either way; not measured)
 #endif
 #ifndef RT_BOX_MM                   // slab test as one comparison max(tmin, -sabs) <= min(tmax, cull) (A/B knob)
-#define RT_BOX_MM 0
+#define RT_BOX_MM 1                 // (r04: C4 +0.3 %, sweep +0.6 %)
 #endif
 #ifndef RT_LEAF_BF                  // BVH leaf triangle test without nested branches (A/B knob)
 #define RT_LEAF_BF 0
