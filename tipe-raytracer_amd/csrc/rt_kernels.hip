@@ -91,6 +91,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_LEAF_BF                  // BVH leaf triangle test without nested branches (A/B knob)
 #define RT_LEAF_BF 0
 #endif
+#ifndef RT_QLDS_IR                  // non-BVH queue kernels: incomingLight / rayColor in LDS (A/B knob)
+#define RT_QLDS_IR 0
+#endif
 #ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
 #define RT_TRI_BF 1
 #endif
@@ -2411,9 +2414,12 @@ struct QHit {
 // NT: the scene has no triangles (every hit is a sphere); OP: every material
 // is opaque (host: !(alpha < 0.0001) && !(alpha <= 0.99), so no alpha hole
 // and no refraction branch is ever taken and neither is compiled in)
-template <bool SKY, int AOM, bool NT = false, bool OP = false>
+// IR: incomingLight / rayColor live in the lane's LDS column (slots
+// ACC_SLOTS..+5 of the sums array) instead of twelve VGPRs
+template <bool SKY, int AOM, bool NT = false, bool OP = false, bool IR = false>
 struct QPath {
     V3 o, d, cd, inc, rc;            // cd: the cast's direction (AO casts; else d)
+    double* accp;                    // (IR) the lane's LDS column
     double top_n2, best;
     int i, kind, win, s, state;
     bool chain, ao_cast;
@@ -2422,6 +2428,36 @@ struct QPath {
     double prs;                      // ... and its reflectionStrength
 
     __device__ __forceinline__ V3 cast_dir() const { return AOM == AO_ON ? cd : d; }
+    __device__ __forceinline__ V3 inc_get() const
+    {
+        if (IR) return v3(accp[(ACC_SLOTS + 0) * 256], accp[(ACC_SLOTS + 1) * 256], accp[(ACC_SLOTS + 2) * 256]);
+        return inc;
+    }
+    __device__ __forceinline__ V3 rc_get() const
+    {
+        if (IR) return v3(accp[(ACC_SLOTS + 3) * 256], accp[(ACC_SLOTS + 4) * 256], accp[(ACC_SLOTS + 5) * 256]);
+        return rc;
+    }
+    __device__ __forceinline__ void inc_set(V3 v)
+    {
+        if (IR) {
+            accp[(ACC_SLOTS + 0) * 256] = v.x;
+            accp[(ACC_SLOTS + 1) * 256] = v.y;
+            accp[(ACC_SLOTS + 2) * 256] = v.z;
+        } else {
+            inc = v;
+        }
+    }
+    __device__ __forceinline__ void rc_set(V3 v)
+    {
+        if (IR) {
+            accp[(ACC_SLOTS + 3) * 256] = v.x;
+            accp[(ACC_SLOTS + 4) * 256] = v.y;
+            accp[(ACC_SLOTS + 5) * 256] = v.z;
+        } else {
+            rc = v;
+        }
+    }
 
     // The hit's material (tri_material / sky_material are pure functions of
     // the hit, so a refraction lane recomputes it instead of keeping it live).
@@ -2435,10 +2471,11 @@ struct QPath {
         return tri_material(kp, win, hp, hn);
     }
 
-    __device__ __forceinline__ bool zero_rc(const KParams& kp) const
+    __device__ __forceinline__ static bool zero_rc_of(const KParams& kp, V3 r)
     {
-        return kp.zero_exit && rc.x == 0.0 && rc.y == 0.0 && rc.z == 0.0;
+        return kp.zero_exit && r.x == 0.0 && r.y == 0.0 && r.z == 0.0;
     }
+    __device__ __forceinline__ bool zero_rc(const KParams& kp) const { return zero_rc_of(kp, rc_get()); }
 
     // After a cast (state SM_RESOLVE).  Returns the role for next_ray, or
     // ROLE_NONE; a lane whose path is over gets state SM_CAM (sum added).
@@ -2459,10 +2496,11 @@ struct QPath {
                 occ = occ + att;
             }
             occ = (occ / 1.0) / AO;
-            rc = mulv(rc, v3(occ, occ, occ));
+            const V3 r2 = mulv(rc_get(), v3(occ, occ, occ));
+            rc_set(r2);
             ao_cast = false;
             ++i;                                         // the bounce after the AO cast
-            ended = zero_rc(kp) || i >= kp.B;
+            ended = zero_rc_of(kp, r2) || i >= kp.B;
             if (!ended) {
                 if (pend) {                              // its direction is still to be made
                     role = ROLE_PBOUNCE;
@@ -2536,8 +2574,8 @@ struct QPath {
                         H.refr = true;
                         role = ROLE_BOUNCE;
                     } else {
-                        shade(kp, mat);
-                        if (zero_rc(kp) || i + 1 >= kp.B) {
+                        const V3 nrc = shade(kp, mat);
+                        if (zero_rc_of(kp, nrc) || i + 1 >= kp.B) {
                             ended = true;                // nothing more reaches the sum
                         } else if (AOM == AO_ON && RT_AO_FIRST && (sn & 3u) == 0u) {
                             role = ROLE_AO;              // AO direction first (ROLE_AO above)
@@ -2552,7 +2590,7 @@ struct QPath {
             }
         }
         if (ended) {
-            if (add_inc) acc_add(acc, ACC_RAD, inc);
+            if (add_inc) acc_add(acc, ACC_RAD, inc_get());
             ++s;
             state = SM_CAM;
             role = ROLE_NONE;
@@ -2561,21 +2599,23 @@ struct QPath {
     }
 
     // shading of an opaque surface (main.c:208-234 without the AO cast)
-    __device__ __forceinline__ void shade_with(const KParams& kp, V3 emis, double es, V3 diff)
+    __device__ __forceinline__ V3 shade_with(const KParams& kp, V3 emis, double es, V3 diff)
     {
-        V3 r = rc;
+        V3 r = rc_get();
         if (AOM == AO_ON) {
             const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
             const V3 em = muls(emis, es * 1.5 * AO);
-            inc = inc + mulv(em, r);
+            inc_set(inc_get() + mulv(em, r));
         } else {
             const V3 em = muls(emis, es);
-            inc = inc + mulv(em, r);
+            inc_set(inc_get() + mulv(em, r));
         }
         if (any_above_half(r)) r = mulv(diff, muls(r, 1.3));
-        rc = mulv(diff, r);
+        const V3 nrc = mulv(diff, r);
+        rc_set(nrc);
+        return nrc;
     }
-    __device__ __forceinline__ void shade(const KParams& kp, const Mat& mat) { shade_with(kp, mat.emis, mat.es, mat.diff); }
+    __device__ __forceinline__ V3 shade(const KParams& kp, const Mat& mat) { return shade_with(kp, mat.emis, mat.es, mat.diff); }
 
     // After next_ray gave a bounce lane its diffuse direction dn.
     __device__ __forceinline__ void finish_bounce(const KParams& kp, V3 dn, Stream& st, double* acc, const QHit& H)
@@ -2627,7 +2667,7 @@ struct QPath {
         ++i;
         ended = ended || i >= kp.B;
         if (ended) {                                     // (refraction lanes only) the sample is over
-            acc_add(acc, ACC_RAD, inc);
+            acc_add(acc, ACC_RAD, inc_get());
             ++s;
             state = SM_CAM;
         } else {
@@ -2667,14 +2707,18 @@ template <bool SKY, int AOM, int QB, bool OPQ = false>   // OPQ: (BVH scenes) ev
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QB < 0 ? RT_WAVES_PER_SIMD_QS : RT_WAVES_PER_SIMD_Q)))
 void render_kernel_q(const KParams kp)
 {
-    __shared__ double acc_lds[ACC_SLOTS * 256];
+    constexpr bool QIR = RT_QLDS_IR && QB <= 0;       // incomingLight / rayColor in LDS (non-BVH kernels)
+    __shared__ double acc_lds[(ACC_SLOTS + (QIR ? 6 : 0)) * 256];
     __shared__ uint32_t rng_lds[4 * 256];
     double* acc = acc_lds + threadIdx.x;
     uint32_t* rng = rng_lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
     unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
-    QPath<SKY, AOM, QB < 0, QB == -2 || OPQ> L;
+    QPath<SKY, AOM, QB < 0, QB == -2 || OPQ, QIR> L;
+    L.accp = acc;
     L.o = L.d = L.cd = L.inc = L.rc = v3(0, 0, 0);
+    L.inc_set(v3(0, 0, 0));
+    L.rc_set(v3(0, 0, 0));
     L.top_n2 = 1.0;
     L.best = 0.0;
     L.i = 0; L.kind = HIT_NONE; L.win = -1; L.s = 0;
@@ -2965,8 +3009,8 @@ void render_kernel_q(const KParams kp)
                 L.o = no;
                 L.d = dn;
                 if (AOM == AO_ON) L.cd = dn;
-                L.inc = v3(0, 0, 0);
-                L.rc = v3(1, 1, 1);
+                L.inc_set(v3(0, 0, 0));
+                L.rc_set(v3(1, 1, 1));
                 L.top_n2 = 1.0;
                 L.i = 0;
                 L.chain = true;
