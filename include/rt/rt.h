@@ -199,9 +199,12 @@ void rt_shutdown(void);
 const char* rt_last_error(void);
 /* Name of the render kernel the calling thread's last render launch used
  * ("render_kernel_q<QB=0|3|4>" = the task-queue kernel without a BVH / with
- * a deep / shallow tree, "render_kernel<BVH>" / "render_kernel" = the
- * fixed-grid kernels, "render_kernel_cuda", "render_kernel_f32"); "none"
- * before the first.  Diagnostics and tests. */
+ * a deep / shallow tree; "render_kernel_q<QB=-1>" / "<QB=-2>" = its
+ * sphere-only instantiations (-2: every material opaque); "<QB=3,OP>" = the
+ * deep-tree one for scenes whose every material is opaque;
+ * "render_kernel<BVH>" / "render_kernel" = the fixed-grid kernels,
+ * "render_kernel_cuda", "render_kernel_f32"); "none" before the first.
+ * The choice never changes a result.  Diagnostics and tests. */
 const char* rt_last_render_kernel(void);
 const char* rt_version(void);
 int  rt_device_count(void);
