@@ -92,7 +92,7 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #define RT_LEAF_BF 0
 #endif
 #ifndef RT_QLDS_IR                  // non-BVH queue kernels: incomingLight / rayColor in LDS (A/B knob)
-#define RT_QLDS_IR 0
+#define RT_QLDS_IR 1                // (r04: C2 kernel 97 VGPRs; C2 +2.45 %, C3 +0.8 %)
 #endif
 #ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
 #define RT_TRI_BF 1
