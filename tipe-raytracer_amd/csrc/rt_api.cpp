@@ -825,15 +825,9 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     // tri_material (rt_kernels.hip): the texel's alpha, overridden for
     // material indices 1 (1.0), 3 (0.1) and 4 (0.6); the texel index is
     // clamped into the whole table, so every texel counts
-    // ... and (RT_OPQ_NOEMIT builds) no triangle emits: every texel's
-    // emissionStrength <= 0 (or NaN: main.c's `es > 0` fails) and no
-    // material index 1 (tri_material's emission override, es = 1.85)
-    const auto plain_mat = [&](const DevMat& m) { return opaque_mat(m) && (!RT_OPQ_NOEMIT || !(m.es > 0)); };
-    ds->tri_opaque = std::all_of(texels.begin(), texels.end(), plain_mat);
-    for (int i = 0; i < scene->nbTriangles && ds->tri_opaque; ++i) {
-        const int m = scene->quelMatPourTri[i];
-        if (m == 3 || m == 4 || (RT_OPQ_NOEMIT && m == 1)) ds->tri_opaque = false;
-    }
+    ds->tri_opaque = std::all_of(texels.begin(), texels.end(), opaque_mat);
+    for (int i = 0; i < scene->nbTriangles && ds->tri_opaque; ++i)
+        if (scene->quelMatPourTri[i] == 3 || scene->quelMatPourTri[i] == 4) ds->tri_opaque = false;
     ds->coord_max = coord_max;
     ds->ns = scene->nbSpheres;
     ds->ns_pad = ns_pad;

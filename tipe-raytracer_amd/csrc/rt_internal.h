@@ -66,13 +66,6 @@ enum : int {
 };
 
 // Everything one render launch needs, passed by value as the kernel argument.
-// The opaque queue-kernel instantiations (rt_kernels.hip OPQ) also require
-// non-emissive triangles and leave out a lit triangle's HSL round trip; the
-// host gate (rt_api.cpp tri_opaque) and the kernels read the same knob.
-#ifndef RT_OPQ_NOEMIT
-#define RT_OPQ_NOEMIT 0
-#endif
-
 struct KParams {
     // scene
     const SphGeo* sph;

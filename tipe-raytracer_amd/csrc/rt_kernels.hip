@@ -82,14 +82,8 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_QOPAQUE_BVH              // deep-tree queue kernel for scenes whose every material (spheres, texels,
 #define RT_QOPAQUE_BVH 1            // no material index 3 / 4) is opaque: no hole / refraction code (r04: C4 +2.9 %)
 #endif
-#ifndef RT_QPIN                     // the QB = -2 instantiation also requires a pinned camera (A/B knob)
-#define RT_QPIN 0                   // (r04: no VGPR change, 109 either way; not measured)
-#endif
 #ifndef RT_BOX_MM                   // slab test as one comparison max(tmin, -sabs) <= min(tmax, cull) (A/B knob)
 #define RT_BOX_MM 1                 // (r04: C4 +0.3 %, sweep +0.6 %)
-#endif
-#ifndef RT_LEAF_BF                  // BVH leaf triangle test without nested branches (A/B knob)
-#define RT_LEAF_BF 0
 #endif
 #ifndef RT_QLDS_IR                  // non-BVH queue kernels: incomingLight / rayColor in LDS (A/B knob)
 #define RT_QLDS_IR 1                // (r04: C2 kernel 97 VGPRs; C2 +2.45 %, C3 +0.8 %)
@@ -549,30 +543,6 @@ __device__ __forceinline__ void tri_test(const KParams& kp, int k, const V3 o, c
         g = kp.tri[k];
     }
     const double det = -(d.x * g.nx + d.y * g.ny + d.z * g.nz);
-    if (RT_LEAF_BF && O32) {
-        // the BVH leaf test without nested branches (RT_LEAF_BF): every lane
-        // evaluates the reference's operations; the tie rule reads the
-        // caller's index unconditionally
-        const V3 ao = v3(o.x - g.ax, o.y - g.ay, o.z - g.az);
-        const V3 dao = cross(ao, d);
-        double invDet;
-        if (det <= 0x1p400) invDet = div_core(1.0, det, rcp_refined(det));
-        else invDet = 1 / det;
-        const double dst = (ao.x * g.nx + ao.y * g.ny + ao.z * g.nz) * invDet;
-        double u = (g.acx * dao.x + g.acy * dao.y + g.acz * dao.z) * invDet;
-        double v = -(g.abx * dao.x + g.aby * dao.y + g.abz * dao.z) * invDet;
-        asm volatile("" : "+v"(u), "+v"(v));
-        const double w = 1 - u - v;
-        const int orig = !kp.tri_orig ? k : *(const int*)((const char*)kp.tri_orig + (uint32_t)k * 4u);
-        const bool closer = (dst < best) | ((dst == best) & (kind == HIT_TRI) & (orig < win_orig));
-        if ((det >= 1E-6) & (dst >= eps) & closer & (u >= eps) & (v >= eps) & (w >= eps)) {
-            best = dst;
-            kind = HIT_TRI;
-            win = k;
-            win_orig = orig;
-        }
-        return;
-    }
     if (det >= 1E-6) {
         const V3 ao = v3(o.x - g.ax, o.y - g.ay, o.z - g.az);
         const V3 dao = cross(ao, d);
@@ -2540,8 +2510,7 @@ struct QPath {
             if (chain) {
                 if (mat.es > 0) {                        // direct view of a light, main.c:154-160
                     V3 col;
-                    // (OP: no triangle emits -- the host's gate -- so a lit hit is a sphere)
-                    if ((NT || (RT_OPQ_NOEMIT && OP) || kind == HIT_SPHERE) && !(SKY && win == kp.ns - 1)) {
+                    if ((NT || kind == HIT_SPHERE) && !(SKY && win == kp.ns - 1)) {
                         const double* sd = kp_here()->sph_disp + 3 * win;   // (host: the same round trip)
                         col = v3(sd[0], sd[1], sd[2]);
                     } else {
@@ -2988,7 +2957,7 @@ void render_kernel_q(const KParams kp)
                 const V3 cc = v3(U[b + U_CAM_C], U[b + U_CAM_C + 1], U[b + U_CAM_C + 2]);
                 const V3 dir = cc + (muls(ch, u) + (muls(cv, v) - co));     // get_ray, camera.h:42-55
                 const V3 dest = co + muls(dir, U[b + U_FOCUS]);
-                if ((RT_QPIN && QB == -2) || kp.cam_pin) {     // zero aperture: the origin itself (host-checked)
+                if (kp.cam_pin) {                              // zero aperture: the origin itself (host-checked)
                     no = co;
                 } else {
                     const double jx = -0.5 + 1.0 * unit31(w.next31());
@@ -3326,7 +3295,7 @@ int launch_render(const KParams& kp, void* stream)
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
-        if (!qbvh) qb = RT_QSPHERES && kp.nt == 0 ? (RT_QOPAQUE && kp.opaque && (!RT_QPIN || kp.cam_pin) ? -2 : -1) : 0;
+        if (!qbvh) qb = RT_QSPHERES && kp.nt == 0 ? (RT_QOPAQUE && kp.opaque ? -2 : -1) : 0;
         const bool opq = RT_QOPAQUE_BVH && qb == 3 && kp.opaque_all;
         t_last_kernel = qb == 3   ? (opq ? "render_kernel_q<QB=3,OP>" : "render_kernel_q<QB=3>")
                         : qb == 4 ? "render_kernel_q<QB=4>"
