@@ -88,6 +88,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_QLDS_IR                  // non-BVH queue kernels: incomingLight / rayColor in LDS (A/B knob)
 #define RT_QLDS_IR 1                // (r04: C2 kernel 97 VGPRs; C2 +2.45 %, C3 +0.8 %)
 #endif
+#ifndef RT_QLDS_INC_BVH             // the opaque deep-tree kernel keeps incomingLight in LDS (A/B knob)
+#define RT_QLDS_INC_BVH 1           // (r04: spills 4 -> 0, C4 +0.7 %)
+#endif
 #ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
 #define RT_TRI_BF 1
 #endif
@@ -2386,7 +2389,7 @@ struct QHit {
 // and no refraction branch is ever taken and neither is compiled in)
 // IR: incomingLight / rayColor live in the lane's LDS column (slots
 // ACC_SLOTS..+5 of the sums array) instead of twelve VGPRs
-template <bool SKY, int AOM, bool NT = false, bool OP = false, bool IR = false>
+template <bool SKY, int AOM, bool NT = false, bool OP = false, int IR = 0>   // IR 1: incomingLight only
 struct QPath {
     V3 o, d, cd, inc, rc;            // cd: the cast's direction (AO casts; else d)
     double* accp;                    // (IR) the lane's LDS column
@@ -2405,7 +2408,7 @@ struct QPath {
     }
     __device__ __forceinline__ V3 rc_get() const
     {
-        if (IR) return v3(accp[(ACC_SLOTS + 3) * 256], accp[(ACC_SLOTS + 4) * 256], accp[(ACC_SLOTS + 5) * 256]);
+        if (IR == 2) return v3(accp[(ACC_SLOTS + 3) * 256], accp[(ACC_SLOTS + 4) * 256], accp[(ACC_SLOTS + 5) * 256]);
         return rc;
     }
     __device__ __forceinline__ void inc_set(V3 v)
@@ -2420,7 +2423,7 @@ struct QPath {
     }
     __device__ __forceinline__ void rc_set(V3 v)
     {
-        if (IR) {
+        if (IR == 2) {
             accp[(ACC_SLOTS + 3) * 256] = v.x;
             accp[(ACC_SLOTS + 4) * 256] = v.y;
             accp[(ACC_SLOTS + 5) * 256] = v.z;
@@ -2676,8 +2679,10 @@ template <bool SKY, int AOM, int QB, bool OPQ = false>   // OPQ: (BVH scenes) ev
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QB < 0 ? RT_WAVES_PER_SIMD_QS : RT_WAVES_PER_SIMD_Q)))
 void render_kernel_q(const KParams kp)
 {
-    constexpr bool QIR = RT_QLDS_IR && QB <= 0;       // incomingLight / rayColor in LDS (non-BVH kernels)
-    __shared__ double acc_lds[(ACC_SLOTS + (QIR ? 6 : 0)) * 256];
+    // incomingLight / rayColor in LDS: both for the non-BVH kernels, incomingLight
+    // alone for the opaque deep-tree kernel (its stack leaves room for 3 doubles)
+    constexpr int QIR = RT_QLDS_IR && QB <= 0 ? 2 : (RT_QLDS_INC_BVH && QB == 3 && OPQ) ? 1 : 0;
+    __shared__ double acc_lds[(ACC_SLOTS + 3 * QIR) * 256];
     __shared__ uint32_t rng_lds[4 * 256];
     double* acc = acc_lds + threadIdx.x;
     uint32_t* rng = rng_lds + threadIdx.x;
