@@ -321,7 +321,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     uni[U_AO] = AO;
     uni[U_WM1] = (double)(p->largeur_image - 1);    // main.c:265 (largeur_image-1)
     uni[U_HM1] = (double)(p->hauteur_image - 1);
-    uni[U_RC_WM1] = uni[U_RC_HM1] = uni[U_RC_AO] = 0.0;   // refined on the device (set_uniforms_kernel)
+    uni[U_RC_WM1] = uni[U_RC_HM1] = 0.0;            // refined on the device (set_uniforms_kernel)
     kp.useAO = p->useAO ? 1 : 0;
     kp.key0 = (uint32_t)p->seed;
     kp.key1 = (uint32_t)(p->seed >> 32);

@@ -62,7 +62,6 @@ enum : int {
     U_CAM_O = 0, U_CAM_H = 3, U_CAM_V = 6, U_CAM_C = 9,
     U_FOCUS = 12, U_OX, U_OY, U_AO, U_WM1, U_HM1,
     U_RC_WM1, U_RC_HM1,      // rcp_refined(W-1), rcp_refined(H-1) (device-computed), or 0: plain division
-    U_RC_AO,                 // rcp_refined(AO) (device-computed) for AO in [2^-400, 2^400], or 0
     U_COUNT
 };
 

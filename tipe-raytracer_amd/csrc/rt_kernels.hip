@@ -91,9 +91,6 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_QLDS_INC_BVH             // the opaque deep-tree kernel keeps incomingLight in LDS (A/B knob)
 #define RT_QLDS_INC_BVH 1           // (r04: spills 4 -> 0, C4 +0.7 %)
 #endif
-#ifndef RT_AO_CORES                 // the queue kernel's AO tail on the exact sqrt / division cores (A/B knob)
-#define RT_AO_CORES 0
-#endif
 #ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
 #define RT_TRI_BF 1
 #endif
@@ -2466,24 +2463,12 @@ struct QPath {
             if (kind != HIT_NONE) {
                 const V3 hp = o + muls(cast_dir(), best);
                 const V3 df = hp - o;
-                const double n2 = dot(df, df);
-                double att;
-                // RT_AO_CORES: sqrt and the division on the exact cores (§4 "Exact
-                // sqrt/division") where their guards hold: |df|^2 in [2^-760, 2^760]
-                // puts distance in [2^-380, 2^380], best in [2^-400, 2^400]
-                if (RT_AO_CORES && n2 >= 0x1p-760 && n2 <= 0x1p760 && best >= 0x1p-400 && best <= 0x1p400) {
-                    att = div_core(sqrt_core(n2), best, rcp_refined(best));
-                } else {
-                    const double distance = sqrt(n2);
-                    att = distance / best;
-                }
+                const double distance = sqrt(dot(df, df));
+                double att = distance / best;
                 att = pm_pow(att, AO);
                 occ = occ + att;
             }
-            occ = occ / 1.0;
-            const double rcAO = ((cdptr)kp.uni)[opq0() + U_RC_AO];
-            const bool occ_ok = occ == 0.0 || (fabs(occ) >= 0x1p-900 && fabs(occ) <= 0x1p900);   // div_core0's range
-            occ = RT_AO_CORES && rcAO != 0.0 && occ_ok ? div_core0(occ, AO, rcAO) : occ / AO;
+            occ = (occ / 1.0) / AO;
             const V3 r2 = mulv(rc_get(), v3(occ, occ, occ));
             rc_set(r2);
             ao_cast = false;
@@ -3101,10 +3086,6 @@ __global__ void set_uniforms_kernel(const UniBlock u, double* __restrict__ dst)
         if (i == U_RC_WM1 || i == U_RC_HM1) {
             const double d = u.v[i == U_RC_WM1 ? U_WM1 : U_HM1];
             v = (d >= 1.0 && d <= 0x1p400) ? rcp_refined(d) : 0.0;
-        }
-        if (i == U_RC_AO) {
-            const double d = u.v[U_AO];
-            v = (d >= 0x1p-400 && d <= 0x1p400) ? rcp_refined(d) : 0.0;
         }
         dst[i] = v;
     }
