@@ -29,12 +29,17 @@ def _zero_some(rng, c, zeros):
     return tuple(0.0 if rng.random() < 0.35 else float(x) for x in c)
 
 
-def random_scene(seed, zeros=False, chunks=None, nt_range=None, spp=None):
+def random_scene(seed, zeros=False, chunks=None, nt_range=None, spp=None, opaque=False, mesh_p=0.7):
+    """opaque: only opaque materials (no glass or hole spheres, texels at
+    alpha 1, no material index 3 or 4), the scenes the queue kernel's
+    opaque instantiations take (QB -2, the deep-tree OPQ kernel);
+    mesh_p: probability of a mesh when nt_range is None."""
     rng = np.random.default_rng(seed)
     ns = int(rng.integers(1, 14))
     sph = (Sphere * ns)()
     for k in range(ns):
-        kind = rng.choice(["diffuse", "mirror", "glass", "hole", "light", "big"])
+        kind = rng.choice(["diffuse", "mirror", "light", "big"] if opaque
+                          else ["diffuse", "mirror", "glass", "hole", "light", "big"])
         c = rng.uniform([-2, -2, -6], [2, 2, -1])
         r = rng.uniform(0.2, 1.2)
         diff = _zero_some(rng, tuple(rng.uniform(0, 1, 3)), zeros)
@@ -53,13 +58,13 @@ def random_scene(seed, zeros=False, chunks=None, nt_range=None, spp=None):
         sph[k].radius = r
         sph[k].mat = scenes.material(diff, em, es, refl, alpha, ior)
     mesh = None
-    if nt_range is not None or rng.random() < 0.7:
+    if nt_range is not None or rng.random() < mesh_p:
         nt = int(rng.integers(40, 120)) if seed % 2 else int(rng.integers(1, 20))
         if nt_range is not None:
             nt = int(rng.integers(*nt_range))
         tris = (Triangle * nt)()
         nm, tw, th = 5, int(rng.integers(1, 5)), int(rng.integers(1, 5))
-        qm = (C.c_int * nt)(*[int(x) for x in rng.integers(0, nm, nt)])
+        qm = (C.c_int * nt)(*[int(x) for x in (rng.choice([0, 1, 2], nt) if opaque else rng.integers(0, nm, nt))])
         for k in range(nt):
             A = rng.uniform([-2, -2, -5], [2, 2, -1.5])
             e = rng.normal(size=(2, 3)) * 0.5
@@ -68,7 +73,7 @@ def random_scene(seed, zeros=False, chunks=None, nt_range=None, spp=None):
         mats = (Material * (nm * tw * th))()
         for k in range(nm * tw * th):
             mats[k] = scenes.material(_zero_some(rng, tuple(rng.uniform(0, 1, 3)), zeros), (0, 0, 0), 0.0, 0.0,
-                                      float(rng.choice([0.0, 0.5, 1.0, 0.7])), 0.0)
+                                      1.0 if opaque else float(rng.choice([0.0, 0.5, 1.0, 0.7])), 0.0)
         mesh = (tris, qm, mats, tw, th, nm)
     bundle = helpers.SceneBundle(sph, mesh)
     cam = tipe_rt.init_camera(tuple(rng.uniform(-0.5, 0.5, 3)), tuple(rng.uniform([-1, -1, -4], [1, 1, -2])),
@@ -125,3 +130,30 @@ def test_random_bvh_scene_queue_tiny_grid_bitexact(seed, monkeypatch):
                              spp=40 + 8 * (seed % 2))
     p.largeur_image, p.hauteur_image = min(p.largeur_image, 20), min(p.hauteur_image, 15)
     check_parity(bundle, p)
+
+
+@pytest.mark.parametrize("seed", range(400, 432))
+def test_random_opaque_sphere_scene_queue_bitexact(seed):
+    """Opaque sphere-only random scenes (r04's QB -2 queue instantiation: no
+    triangle, hole or refraction code) at spp_chunks 2-5, zero-throughput
+    colours on odd seeds; the kernel taken is checked, bit for bit vs the
+    oracle."""
+    bundle, p = random_scene(seed, zeros=bool(seed % 2), chunks=2 + seed % 4, opaque=True, mesh_p=0.0)
+    check_parity(bundle, p)
+    assert tipe_rt.last_render_kernel() == "render_kernel_q<QB=-2>"
+
+
+@pytest.mark.parametrize("seed", range(500, 516))
+def test_random_opaque_bvh_scene_queue_bitexact(seed, monkeypatch):
+    """Opaque random 100-400 triangle scenes through the BVH queue kernel
+    (the deep-tree OPQ instantiation where the tree is deep) on a 1-3 block
+    grid, bit for bit vs the oracle."""
+    monkeypatch.setenv("RT_QUEUE_BLOCKS", str(1 + seed % 3))
+    bundle, p = random_scene(seed, zeros=bool(seed % 2), chunks=5 + seed % 2, nt_range=(100, 400),
+                             spp=40 + 8 * (seed % 2), opaque=True)
+    p.largeur_image, p.hauteur_image = min(p.largeur_image, 20), min(p.hauteur_image, 15)
+    check_parity(bundle, p)
+    # deep trees take the OPQ kernel; shallow ones QB 4; a camera outside the
+    # scene bound the brute-force scan (QB 0); an over-deep tree the fixed grid
+    assert tipe_rt.last_render_kernel() in ("render_kernel_q<QB=3,OP>", "render_kernel_q<QB=4>",
+                                            "render_kernel_q<QB=0>", "render_kernel<BVH>")

@@ -31,6 +31,13 @@ def family_cases(name, seed):
             scenes.with_cuda_materials(bundle.mesh)
         p.semantics = tipe_rt.types.RT_SEM_CUDA
         return (bundle, p), None
+    if name == "opaque_spheres_queue":
+        return random_scene(seed, zeros=bool(seed % 2), chunks=2 + seed % 4, opaque=True, mesh_p=0.0), None
+    if name == "opaque_bvh_queue_tiny_grid":
+        bundle, p = random_scene(seed, zeros=bool(seed % 2), chunks=5 + seed % 2, nt_range=(100, 400),
+                                 spp=40 + 8 * (seed % 2), opaque=True)
+        p.largeur_image, p.hauteur_image = min(p.largeur_image, 20), min(p.hauteur_image, 15)
+        return (bundle, p), str(1 + seed % 3)
     if name == "bvh_queue_tiny_grid":
         bundle, p = random_scene(seed, zeros=bool(seed % 2), chunks=5 + seed % 2, nt_range=(100, 400),
                                  spp=40 + 8 * (seed % 2))
@@ -43,7 +50,8 @@ def main():
     out = sys.argv[1]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     first = int(sys.argv[3]) if len(sys.argv) > 3 else 10000
-    fams = ["random", "zero_throughput_queue", "cuda_semantics", "bvh_queue_tiny_grid"]
+    fams = os.environ.get("FUZZ_FAMILIES", "random,zero_throughput_queue,cuda_semantics,bvh_queue_tiny_grid,"
+                          "opaque_spheres_queue,opaque_bvh_queue_tiny_grid").split(",")
     res = {"families": {}, "first_seed": first, "scenes_per_family": n, "failures": []}
     t0 = time.time()
     for fi, fam in enumerate(fams):
