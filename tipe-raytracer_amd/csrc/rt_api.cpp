@@ -150,7 +150,7 @@ struct rt_device_scene {
     double* sph_disp = nullptr;      // hsl round trip of each sphere's emission
     int sky_w = 0, sky_h = 0;
     int* tri_orig = nullptr;         // leaf order -> caller's triangle index
-    int bvh_nodes = 0, bvh_depth = 0;
+    int bvh_nodes = 0, bvh_depth = 0, bvh_stack4 = 0;
     double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0;
     float bvh_rbox = 0.0f;           // >= every |bound| of the BVH's boxes
     bool mats_bounded = false;       // every diffuse/emission/strength finite, |x| <= 2^100
@@ -356,8 +356,10 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
         kp.bvh_srel = sc->s_rel;
         kp.bvh_sabs = sc->s_abs;
         kp.bvh_rbox = sc->bvh_rbox;
-        // the queue kernel's uint16 stack entries: node index, or 0x8000 | triangle
-        kp.bvh_stack = (sc->bvh_nodes < 0x8000 && sc->nt <= 0x8000) ? 3 * sc->bvh_depth + 1 : 1 << 30;
+        // the traversal stack's uint16 entries (node indices): entries the tree can
+        // need (rt_bvh.cpp's exact bound), or more than any stack when an index
+        // would not fit
+        kp.bvh_stack = (sc->bvh_nodes < 0x8000 && sc->nt <= 0x8000) ? sc->bvh_stack4 : 1 << 30;
         // shallow trees finish most walks in one round with 4 visits; deeper ones
         // do best with 3 (measured: sweep depth4 3: 3395 -> 3542 at 4; C4 depth4 7:
         // 1134 at 3, 1122 at 4)
@@ -841,6 +843,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->sky_h = scene->sky_mat_list ? scene->sky_height : 0;
     ds->bvh_nodes = (int)bvh.nodes4.size();
     ds->bvh_depth = bvh.depth4;
+    ds->bvh_stack4 = bvh.stack4;
     ds->s_rel = bvh.s_rel;
     ds->s_abs = bvh.s_abs;
     ds->r_scene = bvh.r_scene;

@@ -2,8 +2,8 @@
 // (the reference scans every triangle, main.c:80-90, and
 // its CUDA path only has a per-mesh slab box, triangle.hu:42-59).
 //
-// Binary BVH, binned SAH (16 bins on the widest centroid axis), one triangle
-// per leaf (kLeaf; more only at the depth cap or for identical centroids).  Each node stores the boxes
+// Binary BVH, full-sweep SAH over the three axes, one triangle per leaf
+// (kLeaf; more only at the depth cap).  Each node stores the boxes
 // of BOTH children (float, rounded outward), so one 64-byte node fetch
 // decides both descents.  Node 0
 // is the root split; triangles are reordered into leaf order and the kernel
@@ -85,7 +85,6 @@ float up(double x)
     float f = (float)x;
     return (double)f < x ? std::nextafter(f, HUGE_VALF) : f;
 }
-constexpr int kBins = 16;
 
 struct Builder {
     std::vector<Prim>& P;
@@ -94,79 +93,54 @@ struct Builder {
 
     Ref leaf(int b, int e, const Box& box) { return Ref{true, b, e - b, box}; }
 
-    // SAH split position in [b, e) after partitioning, or -1.
-    int split(int b, int e, const Box& cbox, int depth)
+    // Full-sweep SAH: every axis, every split between centroid-sorted
+    // primitives (ties by index, so the build is deterministic), or -1 at the
+    // depth cap.  Against r01-r04's 16 bins on the widest centroid axis: C4
+    // +1.1 %, sweep scene -0.6 % (profiles/r04_bvh/ab.txt).
+    int split(int b, int e, int depth)
     {
         const int n = e - b;
-        int axis = 0;
-        double ext = -1.0;
-        for (int a = 0; a < 3; ++a)
-            if (cbox.hi[a] - cbox.lo[a] > ext) {
-                ext = cbox.hi[a] - cbox.lo[a];
-                axis = a;
+        if (n <= kLeaf || depth >= kMaxDepth) return -1;
+        std::vector<double> rarea((size_t)n);
+        double best = HUGE_VAL;
+        int best_axis = -1, best_i = -1;
+        for (int a = 0; a < 3; ++a) {
+            std::sort(P.begin() + b, P.begin() + e, [a](const Prim& x, const Prim& y) {
+                return x.c[a] < y.c[a] || (x.c[a] == y.c[a] && x.idx < y.idx);
+            });
+            Box r;
+            for (int i = n - 1; i >= 1; --i) {
+                r.grow(P[(size_t)(b + i)].box);
+                rarea[(size_t)i] = r.area();
             }
-        int mid = -1;
-        if (ext > 0.0) {
-            Box bb[kBins];
-            int bc[kBins] = {0};
-            const double scale = kBins / ext;
-            auto bin_of = [&](const Prim& p) {
-                int k = (int)((p.c[axis] - cbox.lo[axis]) * scale);
-                return k < 0 ? 0 : (k >= kBins ? kBins - 1 : k);
-            };
-            for (int i = b; i < e; ++i) {
-                const int k = bin_of(P[(size_t)i]);
-                bb[k].grow(P[(size_t)i].box);
-                ++bc[k];
-            }
-            double best = HUGE_VAL;
-            int best_k = -1;
-            Box left;
-            int nl = 0;
-            for (int k = 0; k < kBins - 1; ++k) {
-                left.grow(bb[k]);
-                nl += bc[k];
-                Box right;
-                int nr = 0;
-                for (int j = k + 1; j < kBins; ++j) {
-                    right.grow(bb[j]);
-                    nr += bc[j];
-                }
-                if (nl == 0 || nr == 0) continue;
-                const double cost = left.area() * nl + right.area() * nr;
+            Box l;
+            for (int i = 1; i < n; ++i) {              // left = [b, b + i)
+                l.grow(P[(size_t)(b + i - 1)].box);
+                const double cost = l.area() * i + rarea[(size_t)i] * (n - i);
                 if (cost < best) {
                     best = cost;
-                    best_k = k;
+                    best_axis = a;
+                    best_i = i;
                 }
             }
-            Box all;
-            for (int i = b; i < e; ++i) all.grow(P[(size_t)i].box);
-            const bool worth = best_k >= 0 && (n > 2 * kLeaf || best < all.area() * n);
-            if (worth) {
-                auto it = std::partition(P.begin() + b, P.begin() + e,
-                                         [&](const Prim& p) { return bin_of(p) <= best_k; });
-                mid = (int)(it - P.begin());
-                if (mid == b || mid == e) mid = -1;
-            }
         }
-        if (mid < 0 && n > kLeaf && depth < kMaxDepth) {     // degenerate centroids: median on index
-            mid = b + n / 2;
-            std::nth_element(P.begin() + b, P.begin() + mid, P.begin() + e,
-                             [&](const Prim& x, const Prim& y) { return x.c[axis] < y.c[axis]; });
-        }
-        return mid;
+        if (best_axis < 0) return -1;
+        if (best_axis != 2)
+            std::sort(P.begin() + b, P.begin() + e, [a = best_axis](const Prim& x, const Prim& y) {
+                return x.c[a] < y.c[a] || (x.c[a] == y.c[a] && x.idx < y.idx);
+            });
+        return b + best_i;
     }
 
     Ref build(int b, int e, int depth)
     {
-        Box box, cbox;
+        Box box;
         for (int i = b; i < e; ++i) {
             box.grow(P[(size_t)i].box);
-            cbox.grow(P[(size_t)i].c);
         }
         max_depth = std::max(max_depth, depth);
         if (e - b <= kLeaf || depth >= kMaxDepth) return leaf(b, e, box);
-        const int mid = split(b, e, cbox, depth);
+        const int mid = split(b, e, depth);
         if (mid < 0) return leaf(b, e, box);
         const int idx = (int)nodes.size();
         nodes.emplace_back();
@@ -310,7 +284,25 @@ bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
         }
         out.nodes4.swap(bfs);
     }
-    if (3 * out.depth4 + 1 > kStack4 || out.nodes4.size() >= 65535) {
+    // Traversal stack bound: bvh_step (rt_kernels.hip) pushes every hit
+    // internal child but the one it enters, and every entry on the stack was
+    // pushed at an ancestor of the current node, so the stack never holds more
+    // than the maximum over root-to-node paths of sum(internal children - 1).
+    // (Breadth-first order: children after parents.)
+    {
+        std::vector<int> need(out.nodes4.size(), 0);
+        for (size_t i = out.nodes4.size(); i-- > 0;) {
+            int k = 0, m = 0;
+            for (int c = 0; c < 4; ++c)
+                if (out.nodes4[i].count[c] == 0) {
+                    ++k;
+                    m = std::max(m, need[(size_t)out.nodes4[i].child[c]]);
+                }
+            need[i] = std::max(0, k - 1) + m;
+        }
+        out.stack4 = need.empty() ? 0 : need[0];
+    }
+    if (out.stack4 > kStack4 || out.nodes4.size() >= 65535) {
         out = BvhBuild();
         return false;
     }

@@ -64,7 +64,8 @@ struct BvhBuild {
     std::vector<BvhNode4> nodes4;   // collapsed 4-wide tree, node 0 = root
     std::vector<int> order;         // leaf order -> original triangle index
     int depth = 0;                  // binary depth
-    int depth4 = 0;                 // 4-wide depth (stack bound: 3 * depth4 + 1 <= kStack4)
+    int depth4 = 0;                 // 4-wide depth
+    int stack4 = 0;                 // traversal stack entries the tree can need (<= 3 * depth4; <= kStack4)
     double s_rel = 0.0, s_abs = 0.0;   // distance-cull slack (rt_bvh.cpp header)
     double r_scene = 0.0;              // coordinate bound the padding assumed
 };

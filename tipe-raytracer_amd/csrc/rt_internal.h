@@ -89,7 +89,7 @@ struct KParams {
     int sky_w, sky_h;
     double bvh_srel, bvh_sabs;   // distance-cull slack (rt_bvh.cpp)
     float bvh_rbox;              // >= |every bound| of the tree's boxes (single-precision slab margin)
-    int bvh_stack;               // traversal stack entries the tree can need (3 * depth4 + 1)
+    int bvh_stack;               // traversal stack entries the tree can need (rt_bvh.h BvhBuild::stack4)
     int bvh_steps;               // queue kernel: node visits per lane and round (host: by tree depth)
     int bvh_nodes;               // 4-wide nodes (breadth-first order: the top levels first)
     int ns, ns_pad, nt;

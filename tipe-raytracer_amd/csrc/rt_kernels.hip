@@ -628,7 +628,7 @@ __device__ __forceinline__ unsigned short* bvh_stack()
 }
 // The queue kernel's per-lane stack (BVH scenes): [kStackQ][256] uint16, 12 KiB,
 // which keeps the kernel at 4 blocks (16 waves) per CU; trees that could need
-// more entries (3 * depth4 + 1 > kStackQ) render with the fixed-grid kernel.
+// more entries (kp.bvh_stack > kStackQ) render with the fixed-grid kernel.
 // The QB = 4 instantiation serves shallow trees only (depth4 <= 4: at most 13
 // entries) and keeps 14, so its top-node cache and the task table fit the
 // same 40 KiB.
