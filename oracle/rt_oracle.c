@@ -14,14 +14,20 @@
  * Compile with -ffp-contract=off: every + - * / is one IEEE rounding, in
  * the reference's association order.
  *
- * Pinning: the leaf functions (hit_sphere, hit_triangle, tri_uvmapping,
- * camera, optics, pile, HSL, write_color_canva) against the reference's own
- * headers compiled here (oracle/Makefile, tests/golden/kat_leaf.json); the
- * composition of tracer / closest_hit / fill_canva against the reference's
- * config-1 image md5 (sphere-only, no AO).  main.c itself
- * cannot be built here (it includes <OpenImageDenoise/oidn.h>, absent), so
- * the composition of the AO, refraction/IOR-stack, texture and alpha-hole
- * branches is PARITY UNPINNED beyond those leaf KATs.
+ * Pinning (both parts against the reference's own code compiled here):
+ *  - leaf functions (hit_sphere, hit_triangle, tri_uvmapping, camera,
+ *    optics, pile, HSL, write_color_canva) against the reference headers
+ *    (oracle/_ref/libref_leaf.so, tests/golden/kat_leaf.json);
+ *  - the composition — closest_hit / ambient_occlusion / tracer / fill_canva
+ *    (main.c:52-284) and add_col_alb_norm (denoiser.h:23-29) — against those
+ *    line ranges compiled VERBATIM (oracle/build_ref_tracer.sh, sha256-pinned,
+ *    no stub header; oracle/_ref/libref_tracer.so).  GLIBC mode reproduces
+ *    them bit for bit on every plane: config 1 in full (P3 md5
+ *    930550ea86f4b2de4ac3a92726beb976), AO at int 2 and 2.5, translucent and
+ *    alpha-hole spheres, the C3 pyramid, mineways' alpha texels, the C4 tree
+ *    + AO and random scenes (tests/golden/composition.json,
+ *    tests/test_oracle_composition.py).  PHILOX mode runs the same
+ *    composition code with the other stream and the portable math.
  */
 #define _GNU_SOURCE
 #include <math.h>

@@ -6,9 +6,12 @@
  * load liboracle.so.  The product (librt_hip.so) never links or calls it.
  *
  * Pinning: RT_RNG_GLIBC mode (libm + the process' glibc rand()) reproduces
- * the reference's config-1 image bit for bit (md5 recorded in SURVEY.md §6);
- * leaf functions are compared with the reference headers compiled in
- * oracle/_ref (see oracle/Makefile) and with tests/golden fixtures.
+ * the reference's own composition — main.c:22-284 + denoiser.h:11-29
+ * compiled verbatim in oracle/_ref/libref_tracer.so — bit for bit on every
+ * plane (tests/golden/composition.json: config 1 in full, AO, refraction,
+ * textures, alpha holes, the C4 tree, random scenes); leaf functions are
+ * compared with the reference headers compiled in oracle/_ref/libref_leaf.so
+ * and with tests/golden/kat_leaf.json (see oracle/Makefile).
  */
 #ifndef RT_ORACLE_H
 #define RT_ORACLE_H

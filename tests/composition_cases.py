@@ -1,0 +1,159 @@
+"""Scenes that pin the oracle's COMPOSITION (tracer / closest_hit /
+ambient_occlusion / fill_canva, main.c:52-284) against the reference's own
+code compiled here (oracle/_ref/libref_tracer.so, oracle/build_ref_tracer.sh).
+
+TEST INFRASTRUCTURE.  Every case renders in the reference's own stream mode:
+glibc rand() reseeded with srand(1), libm, one thread, running per-pixel sums
+(spp_chunks 1).  Each case names the reference driver that produced its
+fixture:
+
+  fill_canva  the reference's fill_canva itself in one pthread (main.c:446),
+              fed a struct ThreadData (int focus / aperture / AO, main.c:42-43)
+  trace_rows  the same loop nest around the reference's tracer with a double
+              AO intensity (tracer's own parameter type, main.c:118) and the
+              pre-quantisation radiance plane
+
+The oracle renders the same case through oracle_render_rows in RT_RNG_GLIBC
+mode; `compat` selects ThreadData's integer truncation (rt.h
+compat_int_truncation).
+"""
+import ctypes as C
+
+import numpy as np
+
+import helpers
+import oracle_ffi
+from tipe_rt import scenes
+from tipe_rt.types import RT_RNG_GLIBC
+
+PLANES = ("canva", "albedo", "normal", "radiance")
+
+
+class Case:
+    def __init__(self, name, build, W, H, spp, bounces, use_ao=False, ao=0.0, driver="trace_rows",
+                 slow=False, what=""):
+        self.name, self.build, self.W, self.H = name, build, W, H
+        self.spp, self.bounces, self.use_ao, self.ao = spp, bounces, use_ao, ao
+        self.driver, self.slow, self.what = driver, slow, what
+
+    def scene(self):
+        """-> (bundle, params) for the oracle in GLIBC mode."""
+        b = self.build()
+        if isinstance(b, tuple):                 # random scene: (bundle, params)
+            bundle, p = b
+            p.rng = RT_RNG_GLIBC
+            p.spp_chunks = 1
+            return bundle, p
+        p = helpers.params(self.W, self.H, self.spp, self.bounces, use_ao=self.use_ao, ao=self.ao,
+                           rng=RT_RNG_GLIBC, compat=1 if self.driver == "fill_canva" else 0)
+        return b, p
+
+
+def _random(seed):
+    """tests/test_gpu_fuzz.random_scene(seed) inside a black, opaque sphere of
+    radius 1e4 (appended last).  Without it a primary miss leaves the
+    reference's albedo/normal undefined: closest_hit (main.c:54-56) never sets
+    HitInfo.mat / .normal on a miss and tracer (main.c:137-140) reads them, so
+    the reference adds stale stack values (seen on seeds 6 and 11), where the
+    build defines 0.  Secondary misses (main.c:236-238) stay
+    covered by the README-box cases (the box is open towards +z)."""
+    def build():
+        from test_gpu_fuzz import random_scene     # noqa: WPS433 (shared generator)
+        from tipe_rt.types import Sphere, Vec3
+        bundle, p = random_scene(seed)
+        n = len(bundle.spheres)
+        sph = (Sphere * (n + 1))()
+        for k in range(n):
+            sph[k] = bundle.spheres[k]
+        sph[n].center = Vec3(0.0, 0.0, 0.0)
+        sph[n].radius = 1e4
+        sph[n].mat = scenes.material((0, 0, 0), (0, 0, 0), 0.0, 0.0, 1.0, 1.0)
+        return helpers.SceneBundle(sph, bundle.mesh), p
+    return build
+
+
+def _glass():
+    """README box with every sphere translucent (alpha 0.5, IOR 1.5): the
+    IOR stack's enter/exit pairs (pile.h, main.c:169-181) on closed spheres."""
+    return helpers.SceneBundle(scenes.cornell_spheres(alpha=0.5, material_index=1.5))
+
+
+def _holes():
+    """README box plus alpha-hole spheres (alpha 0, main.c:200-206) in front of
+    lit ones: the alpha_depth / is_alpha albedo bookkeeping (main.c:137-150)."""
+    hole = scenes.material((0.8, 0.8, 0.8), (0, 0, 0), 0.0, 0.0, 0.0, 1.0)
+    return helpers.SceneBundle(scenes.cornell_spheres(extra=[((0.0, -0.3, -1.6), 0.45, hole),
+                                                              ((-0.4, 0.6, -1.0), 0.3, hole)]))
+
+
+CASES = [
+    Case("c1_full", helpers.cornell, 400, 300, 100, 5, driver="fill_canva", slow=True,
+         what="BASELINE config 1 itself: README box, 400x300, 100 spp, 5 bounces"),
+    Case("cornell_ao_int2", helpers.cornell, 64, 48, 16, 6, use_ao=True, ao=2.0, driver="fill_canva",
+         what="README box + AO, ThreadData's int AO_intensity 2"),
+    Case("cornell_ao_2p5", helpers.cornell, 64, 48, 16, 6, use_ao=True, ao=2.5,
+         what="README box + AO 2.5 as a double (pow(x, 2.5), 1.5*AO emission)"),
+    Case("glass_spheres", _glass, 64, 48, 16, 6,
+         what="all spheres translucent: refraction + IOR stack enter/exit"),
+    Case("hole_spheres", _holes, 64, 48, 16, 6, use_ao=True, ao=2.0, driver="fill_canva",
+         what="alpha-hole spheres + AO: alpha_depth albedo bookkeeping"),
+    Case("pyramid", helpers.pyramid_scene, 64, 48, 16, 6,
+         what="C3: pyramid mesh, 16x16 water texture, alpha 0.706 refraction"),
+    Case("pyramid_ao_int2", helpers.pyramid_scene, 64, 48, 16, 6, use_ao=True, ao=2.0, driver="fill_canva",
+         what="C3 scene + AO through fill_canva"),
+    Case("mineways", helpers.mineways_scene, 64, 48, 16, 6,
+         what="mineways_tri.obj: 11 textures incl. alpha-hole leaves"),
+    Case("tree_ao_int2", helpers.tree_scene, 64, 48, 16, 8, use_ao=True, ao=2.5, driver="fill_canva",
+         what="C4: 1320-triangle tree + AO 2.5 truncated to 2 by ThreadData (main.c:43), 8 bounces"),
+    Case("tree_ao_2p5", helpers.tree_scene, 48, 36, 8, 8, use_ao=True, ao=2.5,
+         what="C4 scene with AO 2.5 kept as a double"),
+] + [Case("random_%d" % s, _random(s), 0, 0, 0, 0,
+          what="tests/test_gpu_fuzz.random_scene(%d) (aperture, focus, AO, textures, mesh)" % s)
+     for s in range(12)]
+
+BY_NAME = {c.name: c for c in CASES}
+
+
+def oracle_planes(case):
+    bundle, p = case.scene()
+    out = helpers.oracle_render(bundle, p)
+    return out
+
+
+def reference_planes(case):
+    """Render the case through the reference's own compiled composition.
+    Returns None when oracle/_ref/libref_tracer.so is unavailable.
+
+    fill_canva cases run the reference's fill_canva AND the trace_rows loop
+    (same truncated ints) and require the two to agree bit for bit on canva,
+    albedo and normal — the check that trace_rows is fill_canva's loop nest;
+    the radiance plane then comes from trace_rows."""
+    lib = oracle_ffi.ref_tracer()
+    if lib is None:
+        return None
+    bundle, p = case.scene()
+    sc = bundle.scene
+    W, H, S, B = p.largeur_image, p.hauteur_image, p.nbRayonParPixel, p.nbRebondMax
+    out = {k: np.zeros((H, W, 3)) for k in PLANES}
+    cam = p.cam
+    geo = (sc.sphere_list, sc.nbSpheres, sc.triangle_list, sc.nbTriangles, sc.mat_list,
+           sc.tex_width, sc.tex_height, sc.quelMatPourTri, C.byref(cam), W, H, S, B)
+    f, ox, oy, ao = p.focus_distance, p.ouverture_x, p.ouverture_y, p.AO_intensity
+    if p.compat_int_truncation:                 # what oracle_render_rows does with ThreadData's ints
+        f, ox, oy, ao = float(int(f)), float(int(ox)), float(int(oy)), float(int(ao))
+    lib.ref_tracer_srand(1)
+    rc = lib.ref_trace_rows(*geo, f, ox, oy, int(p.useAO), ao, H - 1, 0,
+                            out["canva"].ctypes.data, out["albedo"].ctypes.data, out["normal"].ctypes.data,
+                            out["radiance"].ctypes.data)
+    assert rc == 0, rc
+    if case.driver == "fill_canva":
+        assert p.compat_int_truncation
+        fc = {k: np.zeros((H, W, 3)) for k in PLANES[:3]}
+        lib.ref_tracer_srand(1)
+        rc = lib.ref_fill_canva(*geo, int(p.focus_distance), int(p.ouverture_x), int(p.ouverture_y),
+                                int(p.useAO), int(p.AO_intensity), H - 1, 0,
+                                fc["canva"].ctypes.data, fc["albedo"].ctypes.data, fc["normal"].ctypes.data)
+        assert rc == 0, rc
+        for k in fc:
+            assert fc[k].tobytes() == out[k].tobytes(), "trace_rows != the reference's fill_canva on " + k
+    return out

@@ -16,6 +16,7 @@ from tipe_rt.types import (Vec3, Ray, Material, Sphere, Triangle, Camera, Scene,
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
 REF_SO = os.path.join(ORACLE_DIR, "_ref", "libref_leaf.so")
+REF_TRACER_SO = os.path.join(ORACLE_DIR, "_ref", "libref_tracer.so")
 
 
 class OracleHit(C.Structure):
@@ -25,6 +26,7 @@ class OracleHit(C.Structure):
 
 _oracle = None
 _ref = None
+_ref_tracer = None
 
 
 def build_oracle():
@@ -127,6 +129,31 @@ def ref():
         lib.ref_free.argtypes = [C.c_void_p]
         _ref = lib
     return _ref
+
+
+def ref_tracer():
+    """The reference's own main.c:22-284 + denoiser.h:11-29 compiled verbatim
+    (oracle/build_ref_tracer.sh), or None when /root/reference was absent."""
+    global _ref_tracer
+    if _ref_tracer is None:
+        if not os.path.exists(REF_TRACER_SO):
+            if os.path.exists("/root/reference/main.c"):
+                build_oracle()
+            if not os.path.exists(REF_TRACER_SO):
+                return None
+        lib = C.CDLL(REF_TRACER_SO)
+        P = C.POINTER
+        geo = [P(Sphere), C.c_int, P(Triangle), C.c_int, P(Material), C.c_int, C.c_int, P(C.c_int), P(Camera),
+               C.c_int, C.c_int, C.c_int, C.c_int]
+        lib.ref_fill_canva.argtypes = geo + [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                             C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.ref_fill_canva.restype = C.c_int
+        lib.ref_trace_rows.argtypes = geo + [C.c_double, C.c_double, C.c_double, C.c_int, C.c_double, C.c_int,
+                                             C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.ref_trace_rows.restype = C.c_int
+        lib.ref_tracer_srand.argtypes = [C.c_uint]
+        _ref_tracer = lib
+    return _ref_tracer
 
 
 def counters():
