@@ -16,7 +16,11 @@ in float32, so 12 B/px -- SURVEY §8(e)'s float3 colour payload; `--gather
 all` sends canva + albedo + normal as doubles, 72 B/px, for a denoiser) is
 gathered to rank 0 over RCCL (torch.distributed.gather, backend "nccl") and
 rank 0 un-permutes it (rt_assemble_async): total work per step is fixed, so
-scaling is "strong".  At N > 1 rank 0 also times `single_process`: the
+scaling is "strong".  At N > 1 the line's `configs` then holds BASELINE
+configs 3-5 (pyramid; tree + AO; the 4K pyramid frame) at their full spp,
+row-tiled over the same N ranks with the same RCCL gather (configs_sharded:
+Msamples/s, ms per frame, gather ms, per-rank render spread).  At N > 1 rank
+0 also times `single_process`: the
 library's own one-process multi-device frame (rt_render_gather_async over
 the N devices, peer copies over xGMI), the path a C caller of rt.h uses.
 
@@ -311,6 +315,116 @@ def fp32_extra(dev, stream, cam, spheres):
     return out
 
 
+# ---- C3 / C4 / C5 row-tiled over the N ranks (N > 1) -------------------------
+def _max_over_ranks(x, dev, backend):
+    t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def configs_sharded(args, rank, world, dev, cam, names):
+    """BASELINE configs 3-5 at N > 1 (config 4 is quoted on 4 GPUs, config 5
+    on 8 with an RCCL gather; BASELINE.md §4 asks for every config at every
+    N): each rank renders its cyclic 1-row tiles of the config's full frame
+    (rt_render_async with rt.h's cyclic rt_tiling; the reference's row bands,
+    main.c:404-453, and main_cuda.cu:280-339's single-GPU staging are what
+    this replaces), the canva plane travels to rank 0 as float32 over RCCL
+    (torch.distributed.gather) and rank 0 un-permutes it (rt_assemble_async).
+    One frame is timed per config after a short warm-up frame, bracketed by
+    barrier + synchronize, max over ranks; `gather_ms` times the gather +
+    assembly alone in a second bracket.  `--config-spp` reduces the spp (for
+    tests); `--verify` re-renders the frame on rank 0 alone and compares."""
+    out = {}
+    gpu = dev.index
+    st = torch.cuda.current_stream(dev)
+    for name in names:
+        kind, _, bounces, ao, w, h, full_spp, gpus = CONFIGS[name]
+        spp = args.config_spp or full_spp
+        sc, ns, nt = config_scene(kind)
+        ds = tipe_rt.DeviceScene(sc, gpu)
+        tiling = tipe_rt.cyclic_tiling(h, TILE_ROWS, rank, world)
+        rows = tiling.n_tiles * TILE_ROWS
+        p = tipe_rt.make_params(w, h, spp, bounces, cam, focus=3.0, use_ao=ao, ao=2.5, seed=SEED,
+                                chunks=tipe_rt.RT_SPP_CHUNKS_AUTO)
+        local = torch.empty((rows, w, 3), dtype=torch.float64, device=dev)
+        send = torch.empty((1, rows, w, 3), dtype=torch.float32, device=dev)
+        gathered = g64 = full = gather_list = None
+        if rank == 0:
+            gathered = torch.empty((world, 1, rows, w, 3), dtype=torch.float32, device=dev)
+            gather_list = [gathered[r] for r in range(world)]
+            g64 = torch.empty_like(gathered, dtype=torch.float64)
+            full = torch.empty((h, w, 3), dtype=torch.float64, device=dev)
+
+        def gather():
+            if args.dist_backend == "nccl":
+                dist.gather(send, gather_list, dst=0)
+            else:
+                host = [torch.empty_like(send, device="cpu") for _ in range(world)] if rank == 0 else None
+                dist.gather(send.cpu(), host, dst=0)
+                if rank == 0:
+                    for r in range(world):
+                        gathered[r].copy_(host[r])
+            if rank == 0:
+                g64.copy_(gathered)
+                tipe_rt.assemble_async(g64[0, 0].data_ptr(), world, TILE_ROWS, rows, w, h, full.data_ptr(),
+                                       st.cuda_stream, rank_stride=rows * w)
+
+        def frame(pp):
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record(st)
+            tipe_rt.render_async(ds, pp, tiling, local.data_ptr(), stream=st.cuda_stream)
+            ev1.record(st)
+            send[0].copy_(local)                      # canva integers, exact in float32
+            gather()
+            return ev0, ev1
+
+        long_frame = w * h * spp >= 2e9
+        warm = p if not long_frame else tipe_rt.make_params(w, h, 8, bounces, cam, focus=3.0, use_ao=ao, ao=2.5,
+                                                             seed=SEED, chunks=tipe_rt.RT_SPP_CHUNKS_AUTO)
+        frame(warm)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ev0, ev1 = frame(p)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        elapsed = _max_over_ranks(time.perf_counter() - t0, dev, args.dist_backend)
+        render_ms = ev0.elapsed_time(ev1)
+        render_ms_max = _max_over_ranks(render_ms, dev, args.dist_backend)
+        render_ms_min = -_max_over_ranks(-render_ms, dev, args.dist_backend)
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        gather()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        gather_s = _max_over_ranks(time.perf_counter() - t1, dev, args.dist_backend)
+        rec = {"n_gpus": world, "msamples_per_s": round(w * h * spp / elapsed / 1e6, 1),
+               "ms_per_frame": round(elapsed * 1e3, 3), "gather_ms": round(gather_s * 1e3, 3),
+               "rank_render_ms_max": round(render_ms_max, 3), "rank_render_ms_min": round(render_ms_min, 3),
+               "spp": spp, "full_spp": full_spp, "width": w, "height": h, "bounces": bounces, "ao": ao,
+               "spheres": ns, "triangles": nt, "config_gpus": gpus, "tile_rows": TILE_ROWS,
+               "rows_per_rank": rows, "frames_timed": 1, "warmup_spp": warm.nbRayonParPixel,
+               "collective": "rccl gather" if args.dist_backend == "nccl" else "gloo gather (host)",
+               "gather_payload": "canva as float32, 12 B/px", "scaling": "strong"}
+        if args.verify and rank == 0:
+            ref = torch.empty((h, w, 3), dtype=torch.float64, device=dev)
+            tipe_rt.render_async(ds, p, tipe_rt.band_tiling(0, h - 1), ref.data_ptr(), stream=st.cuda_stream)
+            torch.cuda.synchronize(dev)
+            rec["verified_vs_single_device"] = bool(torch.equal(ref, full))
+            if not rec["verified_vs_single_device"]:
+                print("verify: %s assembled frame differs from the single-device frame" % name, file=sys.stderr)
+            del ref
+        dist.barrier()
+        ds.close()
+        del local, send, gathered, g64, full
+        torch.cuda.empty_cache()
+        out[name] = rec
+    return out
+
+
 # ---- end-to-end host-buffer rates of the drop-ins (N = 1) --------------------
 def end_to_end(scene, spheres, cam, reps=2):
     """Upload -> render -> assembled host framebuffer through the C-ABI:
@@ -485,6 +599,11 @@ def main():
                          "nccl (= RCCL) is the measured configuration")
     ap.add_argument("--no-single-process", action="store_true",
                     help="N>1: skip the single_process leg (rt_render_gather_async over the N devices)")
+    ap.add_argument("--configs", default="C3,C4,C5",
+                    help="N>1: BASELINE configs rendered row-tiled over the N ranks after the C2 headline "
+                         "(comma list of C3, C4, C5; empty: none)")
+    ap.add_argument("--config-spp", type=int, default=0,
+                    help="N>1 config legs: render at this spp instead of each config's full spp (tests)")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -621,6 +740,16 @@ def main():
         dist.barrier(group=cpu_group)
         torch.cuda.set_device(dev)
 
+    # --- C3 / C4 / C5 row-tiled over the N ranks ------------------------------
+    sharded = None
+    if world > 1 and args.configs:
+        names = [n.strip() for n in args.configs.split(",") if n.strip()]
+        bad = [n for n in names if n not in ("C3", "C4", "C5")]
+        if bad:
+            raise SystemExit("bench.py: unknown --configs %s" % bad)
+        sharded = configs_sharded(args, rank, world, dev, cam, names)
+        torch.cuda.set_device(dev)
+
     # --- kernel-only timing with HIP events on the launch stream ------------
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     n_k = max(1, min(args.steps, 3))
@@ -710,6 +839,8 @@ def main():
                                             for r in range(world)})
         if single is not None:
             rec["single_process"] = single
+        if sharded is not None:
+            rec["configs"] = sharded
         if world == 1 and not args.no_extras:
             rec["configs"] = configs_extra(dev, stream, cam)
             rec["end_to_end"] = end_to_end(scene, spheres, cam)

@@ -29,8 +29,11 @@ extern "C" {
 /* 2: rt_params gained `precision` (RT_PREC_*) and rt_params_init defaults
  *    spp_chunks to RT_SPP_CHUNKS_AUTO (a different summation grouping than
  *    the strict fill_canva order of spp_chunks = 1); build rt_params with
- *    rt_params_init so new fields read their defaults.  rt_gather_async.  */
-#define RT_ABI_VERSION 2
+ *    rt_params_init so new fields read their defaults.  rt_gather_async.
+ * 3: RT_CNT_BVH_STACK_OVER appended (RT_NCOUNTERS 17 -> 18): d_counters
+ *    arrays of rt_count_async hold RT_NCOUNTERS entries; scenes above 65534
+ *    spheres upload (exact sphere scans) instead of RT_EUNSUPPORTED.      */
+#define RT_ABI_VERSION 3
 
 /* ---- status codes ------------------------------------------------------- */
 #define RT_OK            0
@@ -340,6 +343,13 @@ enum {
                              diagnostic; vs casts)                       */
     RT_CNT_SHADE_LANE_SLOTS, /* 64 x wave-level hit resolutions (bounce
                              shading or AO tail; GPU diagnostic)         */
+    RT_CNT_BVH_STACK_OVER, /* BVH stack pushes made at a depth >= the LDS
+                             stack of the kernel that renders this tree
+                             (the queue kernel's 24 / 14 entries, else the
+                             fixed grid's 48).  Must be 0: the host admits a
+                             tree by its exact stack bound (rt_bvh.cpp); a
+                             nonzero count means that bound is wrong (GPU
+                             diagnostic, rt_count_async only)            */
     RT_NCOUNTERS
 };
 /* Same traversal as rt_render_async, no frame; adds event counts into the

@@ -53,9 +53,13 @@ def test_gpus_2_spawns_two_ranks_and_verifies():
     """Two ranks on the one-GPU box (gloo gather through host copies), as the
     8-GPU run does with RCCL: n_gpus must be 2, the assembled frame must equal
     a single-device render bit for bit, and the single-process leg
-    (rt_render_gather_async over both slots) must too."""
+    (rt_render_gather_async over both slots) must too.  The C3 / C4 / C5
+    legs (row-tiled over the ranks at a reduced 2 spp) must each assemble
+    the single-device frame bit for bit -- C4 through the BVH queue kernel
+    on cyclic tiles, C5 at 3840x2880."""
     r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend",
-                        "gloo", "--steps", "1", "--warmup", "0", "--no-extras", "--no-cpu-baseline", "--verify"],
+                        "gloo", "--steps", "1", "--warmup", "0", "--no-extras", "--no-cpu-baseline", "--verify",
+                        "--config-spp", "2"],
                        capture_output=True, text=True, timeout=600, env=_env(), cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
@@ -66,3 +70,9 @@ def test_gpus_2_spawns_two_ranks_and_verifies():
     assert sp["verified_vs_single_device"] is True
     assert len(sp["devices"]) == 2
     assert rec["value"] > 0
+    assert sorted(rec["configs"]) == ["C3", "C4", "C5"]
+    for name, c in rec["configs"].items():
+        assert c["n_gpus"] == 2 and c["spp"] == 2, name
+        assert c["verified_vs_single_device"] is True, name
+        assert c["msamples_per_s"] > 0 and c["gather_ms"] >= 0, name
+    assert rec["configs"]["C5"]["rows_per_rank"] == 1440

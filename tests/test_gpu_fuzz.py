@@ -16,7 +16,7 @@ import helpers
 import tipe_rt
 from tipe_rt import scenes
 from tipe_rt.types import Sphere, Triangle, Material, Vec3, UV
-from test_gpu_parity import check_parity
+from test_gpu_parity import check_parity, assert_stack_bound_holds
 
 pytestmark = pytest.mark.gpu
 
@@ -130,6 +130,7 @@ def test_random_bvh_scene_queue_tiny_grid_bitexact(seed, monkeypatch):
                              spp=40 + 8 * (seed % 2))
     p.largeur_image, p.hauteur_image = min(p.largeur_image, 20), min(p.hauteur_image, 15)
     check_parity(bundle, p)
+    assert_stack_bound_holds(bundle, p)
 
 
 @pytest.mark.parametrize("seed", range(400, 432))
@@ -153,6 +154,7 @@ def test_random_opaque_bvh_scene_queue_bitexact(seed, monkeypatch):
                              spp=40 + 8 * (seed % 2), opaque=True)
     p.largeur_image, p.hauteur_image = min(p.largeur_image, 20), min(p.hauteur_image, 15)
     check_parity(bundle, p)
+    assert_stack_bound_holds(bundle, p)
     # deep trees take the OPQ kernel; shallow ones QB 4; a camera outside the
     # scene bound the brute-force scan (QB 0); an over-deep tree the fixed grid
     assert tipe_rt.last_render_kernel() in ("render_kernel_q<QB=3,OP>", "render_kernel_q<QB=4>",

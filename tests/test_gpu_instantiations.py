@@ -95,3 +95,22 @@ def test_tree_with_override_material_keeps_qb3(mat_index):
     bundle = helpers.SceneBundle(scenes.cornell_spheres(), (tris, qm, mats2, tw, th, n_new))
     p = helpers.params(40, 30, 6, 8, use_ao=True, chunks=4)
     assert render_and_compare(bundle, p) == "render_kernel_q<QB=3>"
+
+
+@pytest.mark.parametrize("scene", ["tree", "sweep", "mineways"])
+def test_bvh_stack_bound_holds_on_the_gpu(scene):
+    """rt_count_async checks every BVH push against the LDS stack of the
+    kernel launch_render picks for the tree (rt.h RT_CNT_BVH_STACK_OVER):
+    the C4 tree (deep-tree queue kernel, 24 entries), the 100-triangle sweep
+    mesh and mineways (606 triangles), over a whole frame with AO."""
+    from test_gpu_parity import assert_stack_bound_holds
+    if scene == "tree":
+        bundle = helpers.tree_scene()
+    elif scene == "mineways":
+        bundle = helpers.mineways_scene()
+    else:
+        sph, mesh = scenes.synthetic_cornell(10, 100)
+        bundle = helpers.SceneBundle(sph, mesh)
+    p = helpers.params(120, 90, 4, 8, use_ao=True, ao=2.5, chunks=4)
+    c = assert_stack_bound_holds(bundle, p)
+    assert c[tipe_rt.types.RT_CNT_BVH_NODES] > 0          # the tree was walked

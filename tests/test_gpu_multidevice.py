@@ -30,14 +30,23 @@ def _slots(n):
     return lib
 
 
-@pytest.mark.parametrize("slots,tile_rows,chunks", [(2, 1, 4), (3, 4, 1), (2, 2, 1)])
-def test_render_gather_slots_bitexact(slots, tile_rows, chunks):
+@pytest.mark.parametrize("slots,tile_rows,chunks,scene", [(2, 1, 4, "pyramid"), (3, 4, 1, "pyramid"),
+                                                          (2, 2, 1, "pyramid"), (2, 1, 4, "tree"),
+                                                          (3, 1, 32, "tree")])
+def test_render_gather_slots_bitexact(slots, tile_rows, chunks, scene):
+    """tree: the C4 scene (1320-triangle BVH + AO 2.5, 8 bounces) through the
+    BVH queue kernel on cyclic 1-row tiles and the gather -- C4's own
+    multi-GPU layout (BASELINE config 4)."""
     import torch
     lib = _slots(slots)
     try:
-        bundle = helpers.pyramid_scene()
         W, H = 52, 41
-        p = helpers.params(W, H, 8, 6, chunks=chunks)
+        if scene == "tree":
+            bundle = helpers.tree_scene()
+            p = helpers.params(W, H, 8 if chunks < 32 else 32, 8, use_ao=True, ao=2.5, chunks=chunks)
+        else:
+            bundle = helpers.pyramid_scene()
+            p = helpers.params(W, H, 8, 6, chunks=chunks)
         ref = helpers.oracle_render(bundle, p)
         planes = torch.full((4, H, W, 3), -2.0, dtype=torch.float64, device="cuda:0")
         st = torch.cuda.current_stream().cuda_stream

@@ -40,6 +40,27 @@ def gpu_render(bundle, p, tiling=None, radiance=True):
     return [b.cpu().numpy() for b in bufs]
 
 
+def gpu_counts(bundle, p):
+    """rt_count_async over the whole frame: the RT_NCOUNTERS event totals."""
+    import torch
+    ds = tipe_rt.DeviceScene(bundle.scene, 0)
+    d = torch.zeros(tipe_rt.RT_NCOUNTERS, dtype=torch.int64, device="cuda:0")
+    tipe_rt.count_async(ds, p, tipe_rt.band_tiling(0, p.hauteur_image - 1), d.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    ds.close()
+    return [int(x) for x in d.cpu()]
+
+
+def assert_stack_bound_holds(bundle, p):
+    """Every BVH push of the frame's walks stays inside the LDS stack of the
+    kernel that renders the tree (rt.h RT_CNT_BVH_STACK_OVER == 0), i.e.
+    the host's stack bound (rt_bvh.cpp) covers the kernel's push rule."""
+    c = gpu_counts(bundle, p)
+    assert c[tipe_rt.types.RT_CNT_BVH_STACK_OVER] == 0, c
+    return c
+
+
 def assert_same(gpu, ref, what):
     """Bit-for-bit equal values; NaN must sit at the same places (payloads
     may differ: x86 and gfx950 produce different default NaNs)."""

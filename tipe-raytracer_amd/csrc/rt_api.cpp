@@ -287,6 +287,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     }
     kp.ns = sc->ns;
     kp.ns_pad = sc->ns_pad;
+    kp.ns_cand = std::isfinite(sc->cand_lmax) ? sc->ns_pad : 0;
     kp.nt = sc->nt;
     kp.tw = sc->tw;
     kp.th = sc->th;
@@ -685,8 +686,9 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
 
     // Spheres padded to an even count with never-hit records (r2 = -inf makes
     // the discriminant -inf): the kernel reads them two per s_load_dwordx16.
-    // the candidate pass keeps the winner's slot in 16 mantissa bits (RT_CAND_TAG)
-    if (scene->nbSpheres > 65534) return fail(RT_EUNSUPPORTED, "%d spheres > 65534", scene->nbSpheres);
+    // The candidate pass keeps the winner's slot in 16 mantissa bits (RT_CAND_TAG):
+    // above 65534 spheres it is switched off (cand_lmax = +inf, KParams::ns_cand = 0)
+    // and every ray takes the exact reference scan -- correct for any count, slower.
     const int ns_pad = (scene->nbSpheres + 1) & ~1;
     std::vector<SphGeo> sph((size_t)ns_pad, SphGeo{0.0, 0.0, 0.0, -HUGE_VAL});
     std::vector<SphCand> cand((size_t)ns_pad, SphCand{0.0, 0.0, 0.0, HUGE_VAL});
@@ -710,7 +712,8 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         sph_rinv[i] = 1 / s.radius;                    // divide(v, t) = v * (1/t), vec3.h:105-107
         hsl_roundtrip_host(s.mat.emissionColor, &sph_disp[3 * (size_t)i]);
     }
-    const double cand_lmax = std::isfinite((double)lmax) ? std::nextafter((double)lmax, HUGE_VAL) : HUGE_VAL;
+    const double cand_lmax = std::isfinite((double)lmax) && scene->nbSpheres <= 65534
+                                 ? std::nextafter((double)lmax, HUGE_VAL) : HUGE_VAL;
     std::vector<DevMat> sky;
     if (scene->sky_mat_list)
         for (long long i = 0; i < (long long)scene->sky_width * scene->sky_height; ++i)
@@ -1502,6 +1505,7 @@ int rt_verify_sphere_pass(const rt_scene* scene, const double* rays, long long n
     kp.cand_lmax = ds->cand_lmax;
     kp.ns = ds->ns;
     kp.ns_pad = ds->ns_pad;
+    kp.ns_cand = std::isfinite(ds->cand_lmax) ? ds->ns_pad : 0;
     double* d_rays = nullptr;
     unsigned long long* d = nullptr;
     hipError_t e = hipMalloc((void**)&d_rays, (size_t)n * 6 * sizeof(double));

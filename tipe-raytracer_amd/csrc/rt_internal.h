@@ -127,6 +127,9 @@ struct KParams {
                              // other fields keep their kernarg offsets (and the kernels their SMEM loads)
     int opaque_all;          // ... and so is every triangle material: every texel, no material index 3 or 4
                              // (tri_material's alpha overrides); the deep-tree OPQ instantiation
+    int ns_cand;             // spheres the candidate pass scans: ns_pad, or 0 when cand_lmax is +inf (every
+                             // ray then takes the exact scan: non-finite spheres, or more than 65534
+                             // spheres, whose slots do not fit RT_CAND_TAG's 16 bits)
 };
 
 struct UniBlock { double v[U_COUNT]; };

@@ -424,7 +424,7 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
     double bn2 = __hiloint2double(0x7fefffff, -1);
     if (MN) bn = bn2;
     double gmin = bn2;                   // (RT_CAND_GACC) min |D| over the scan
-    for (int k = 0; k < kp.ns_pad; k += 2) {
+    for (int k = 0; k < kp.ns_cand; k += 2) {
         double g[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[j] = sc[4 * k + j];
@@ -474,7 +474,7 @@ __device__ __forceinline__ int spheres_closest(const KParams& kp, const V3 o, co
             amb = amb || (valid && (sure != (n >= tM)));    // the chosen root straddles 1e-4
             const bool cand = valid && sure;
             // RT_CAND_TAG: n with its low 16 mantissa bits replaced by the slot
-            // (one v_and_or_b32; host: ns_pad <= 65536); |nt - n| < 2^-36 |n|
+            // (one v_and_or_b32; host: ns_cand <= 65534); |nt - n| < 2^-36 |n|
             // <= 2^-34.4 Hs, inside M's slack
             const double nt = RT_CAND_TAG ? cand_tag(n, k + e, msk) : n;
             const double diff = nt - bn;
@@ -633,6 +633,16 @@ __device__ __forceinline__ unsigned short* bvh_stack()
 // entries) and keeps 14, so its top-node cache and the task table fit the
 // same 40 KiB.
 constexpr int kStackQ = 24, kStackQ4 = 14;
+// The LDS stack entries of the kernel launch_render picks for a tree: the
+// queue kernel's QB = 4 (kStackQ4) or QB = 3 (kStackQ) instantiation, else
+// the fixed-grid kernel (kStack4).  COUNT runs check every push against it
+// (RT_CNT_BVH_STACK_OVER), so a host stack bound that misses the kernel's
+// push rule shows up as a count, not as a neighbour lane's corrupted stack.
+__host__ __device__ inline int stack_cap_of(int bvh_stack, int bvh_steps)
+{
+    if (bvh_stack > kStackQ) return kStack4;
+    return bvh_steps <= 3 || bvh_stack > kStackQ4 ? kStackQ : kStackQ4;
+}
 template <int QB>
 __device__ __forceinline__ unsigned short* bvh_stack_q()
 {
@@ -843,8 +853,11 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
                 next = ch;
                 tnext = tn[c];
             }
-            stk[sp * 256] = (unsigned short)push;
-            ++sp;
+            if (COUNT && sp >= stack_cap_of(kp.bvh_stack, kp.bvh_steps)) cnt.c[RT_CNT_BVH_STACK_OVER] += 1;
+            if (!COUNT || sp < kStack4) {    // COUNT walks use the fixed grid's stack
+                stk[sp * 256] = (unsigned short)push;
+                ++sp;
+            }
         }
     }
     // The triangles of every hit leaf in one loop, one triangle per lane and
@@ -1650,8 +1663,11 @@ __device__ __forceinline__ bool coop_step(const KParams& kp, const V3 o, const V
                 push[npush] = (unsigned)pu;
                 ++npush;
             } else {
-                stk[sp * 256] = (unsigned short)pu;
-                ++sp;
+                if (COUNT && sp >= stack_cap_of(kp.bvh_stack, kp.bvh_steps)) cnt.c[RT_CNT_BVH_STACK_OVER] += 1;
+                if (!COUNT || sp < kStack4) {
+                    stk[sp * 256] = (unsigned short)pu;
+                    ++sp;
+                }
             }
         }
     }
@@ -3293,7 +3309,7 @@ int launch_render(const KParams& kp, void* stream)
     int qb = 0;
     bool qbvh = false;
     if (kp.bvh != nullptr && kp.bvh_stack <= kStackQ) {
-        qb = kp.bvh_steps <= 3 || kp.bvh_stack > kStackQ4 ? 3 : 4;
+        qb = stack_cap_of(kp.bvh_stack, kp.bvh_steps) == kStackQ ? 3 : 4;
         qbvh = qb == 4 || !RT_QNODE_H || kp.bvhh != nullptr;
     }
     if (kp.task_ctr && kp.chunks > 1 && (!kp.bvh || qbvh) && !kp.cuda && !kp.f32 && !kp.sums) {
