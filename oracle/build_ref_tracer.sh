@@ -23,6 +23,10 @@ HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
 REFROOT="${REFROOT:-/root/reference}"
 CC="${CC:-gcc}"
 OUT="$HERE/_ref/libref_tracer.so"
+VARIANT="${1:-glibc}"            # glibc (the reference as shipped) | philox (the GPU's stream spec)
+if [ "$VARIANT" = philox ]; then
+    OUT="$HERE/_ref/libref_tracer_philox.so"
+fi
 
 if [ ! -f "$REFROOT/main.c" ] || [ ! -f "$REFROOT/denoiser.h" ]; then
     echo "build_ref_tracer: $REFROOT absent, skipping" >&2
@@ -50,6 +54,10 @@ mkdir -p "$HERE/_ref"
 {
     printf '#include <stdio.h>\n#include <math.h>\n#include <stdbool.h>\n#include <stdlib.h>\n'
     printf '#include <time.h>\n#include <sys/time.h>\n#include <pthread.h>\n#include <string.h>\n'
+    if [ "$VARIANT" = philox ]; then
+        # rand() -> rt.h's RT_RNG_PHILOX draw; acos/sinf/cosf/pow -> pm_math.h
+        printf '#define REF_STREAM_PHILOX 1\n#include "ref_tracer_stream.h"\n'
+    fi
     printf '#include "vec3.h"\n#include "ray.h"\n#include "hitinfo.h"\n#include "sphere.h"\n'
     printf '#include "rtutility.h"\n#include "camera.h"\n'
     printf '#line 11 "%s/denoiser.h"\n' "$REFROOT"

@@ -37,6 +37,18 @@
  *                     main.c:43) and the pre-quantisation mean radiance
  *                     (sum/S) as a fourth plane.  Its equality with
  *                     ref_fill_canva at integer AO is itself a test.
+ *
+ * With -DREF_STREAM_PHILOX (oracle/_ref/libref_tracer_philox.so) the same
+ * verbatim ranges are compiled with the GPU's stream spec substituted for
+ * the reference's two third-party dependencies, by object-like macros
+ * defined before the reference headers (build_ref_tracer.sh): glibc rand()
+ * becomes draw n of sample s at pixel p of rt.h's RT_RNG_PHILOX stream, and
+ * libm's acos / sinf / cosf / pow become the portable oracle/pm_math.h
+ * functions the kernel implements (sqrt, sqrtf, fmod are correctly rounded
+ * either way).  The reference's own tracer / closest_hit /
+ * ambient_occlusion / hit tests / shading then run the kernel's exact draw
+ * sequence, so the GPU's frames can be compared with the reference's code
+ * directly (ref_trace_rows_philox, tests/golden/gpu_reference.json).
  */
 #include <pthread.h>
 
@@ -114,3 +126,48 @@ EXPORT int ref_trace_rows(const sphere* sph, int ns, const triangle* tris, int n
 }
 
 EXPORT void ref_tracer_srand(unsigned s) { srand(s); }
+
+#ifdef REF_STREAM_PHILOX
+/* ref_trace_rows with the RT_RNG_PHILOX stream keyed by (seed, global pixel
+ * j*W+i, sample x), summing each pixel's samples in rt.h's spp_chunks slices
+ * (rt_chunk_bound: per-slice running sums, then the slice sums in slice
+ * order; P = 1 is fill_canva's running sum). */
+EXPORT int ref_trace_rows_philox(const sphere* sph, int ns, const triangle* tris, int nt, const material* mats,
+                                 int tw, int th, const int* qm, const camera* cam, int W, int H, int spp,
+                                 int bounces, double focus, double ox, double oy, int useAO, double AO,
+                                 unsigned long long seed, int chunks, int row_hi, int row_lo, color* canva,
+                                 color* albedo, color* normal, color* radiance)
+{
+    if (W < 2 || H < 2 || spp < 1) return -1;
+    const int P = rt_resolve_spp_chunks(chunks, spp);
+    ref_ps.seed = seed;
+    for (int j = row_hi; j >= row_lo; --j) {
+        for (int i = 0; i < W; i++) {
+            const int pixel_index = j * W + i;
+            col_alb_norm total = {{BLACK, BLACK, BLACK}};
+            for (int c = 0; c < P; ++c) {
+                col_alb_norm part = {{BLACK, BLACK, BLACK}};
+                const int s0 = (int)rt_chunk_bound(c, spp, P), s1 = (int)rt_chunk_bound(c + 1, spp, P);
+                for (int x = s0; x < s1; ++x) {
+                    ref_ps.pixel = (uint32_t)pixel_index;
+                    ref_ps.sample = (uint32_t)x;
+                    ref_ps.n = 0;
+                    double u = ((double)i + randomDouble(-0.5, 0.5)) / (W - 1);
+                    double v = ((double)j + randomDouble(-0.5, 0.5)) / (H - 1);
+                    double dx = randomDouble(-0.5, 0.5) * ox;
+                    double dy = randomDouble(-0.5, 0.5) * oy;
+                    ray r = get_ray(u, v, *cam, focus, dx, dy);
+                    part = add_col_alb_norm(part, tracer(r, bounces, (sphere*)sph, ns, (triangle*)tris, nt, AO,
+                                                         useAO != 0, (material*)mats, tw, th, (int*)qm, NULL, 0, 0));
+                }
+                total = c == 0 ? part : add_col_alb_norm(total, part);
+            }
+            canva[pixel_index] = write_color_canva(total.e[0], spp);
+            if (albedo) albedo[pixel_index] = divide_scalar(total.e[1], spp);
+            if (normal) normal[pixel_index] = divide_scalar(total.e[2], spp);
+            if (radiance) radiance[pixel_index] = divide_scalar(total.e[0], spp);
+        }
+    }
+    return 0;
+}
+#endif

@@ -157,3 +157,80 @@ def reference_planes(case):
         for k in fc:
             assert fc[k].tobytes() == out[k].tobytes(), "trace_rows != the reference's fill_canva on " + k
     return out
+
+
+def reference_planes_philox(bundle, p):
+    """The reference's own composition with the GPU's stream spec (RT_RNG_PHILOX
+    draws keyed by (seed, pixel, sample); portable acos/sinf/cosf/pow) and
+    p.spp_chunks' slice grouping: what librt_hip.so must produce bit for bit.
+    None when oracle/_ref/libref_tracer_philox.so is unavailable."""
+    lib = oracle_ffi.ref_tracer_philox()
+    if lib is None:
+        return None
+    sc = bundle.scene
+    W, H, S, B = p.largeur_image, p.hauteur_image, p.nbRayonParPixel, p.nbRebondMax
+    out = {k: np.zeros((H, W, 3)) for k in PLANES}
+    cam = p.cam
+    f, ox, oy, ao = p.focus_distance, p.ouverture_x, p.ouverture_y, p.AO_intensity
+    if p.compat_int_truncation:
+        f, ox, oy, ao = float(int(f)), float(int(ox)), float(int(oy)), float(int(ao))
+    rc = lib.ref_trace_rows_philox(sc.sphere_list, sc.nbSpheres, sc.triangle_list, sc.nbTriangles, sc.mat_list,
+                                   sc.tex_width, sc.tex_height, sc.quelMatPourTri, C.byref(cam), W, H, S, B,
+                                   f, ox, oy, int(p.useAO), ao, p.seed, p.spp_chunks, H - 1, 0,
+                                   *[out[k].ctypes.data for k in PLANES])
+    assert rc == 0, rc
+    return out
+
+
+# ---- the GPU's stream spec: cases for tests/golden/gpu_reference.json ------
+class PhiloxCase:
+    """A scene + RT_RNG_PHILOX params; `chunks` picks the kernel family the
+    GPU takes (1: fixed grid; > 1: the persistent queue kernel)."""
+
+    def __init__(self, name, build, W=64, H=48, spp=16, bounces=6, use_ao=False, ao=0.0, compat=1, chunks=32,
+                 seed=1010, what=""):
+        self.name, self.build, self.W, self.H, self.spp, self.bounces = name, build, W, H, spp, bounces
+        self.use_ao, self.ao, self.compat, self.chunks, self.seed, self.what = use_ao, ao, compat, chunks, seed, what
+
+    def scene(self):
+        b = self.build()
+        if isinstance(b, tuple):                 # random scene: its own params, Philox stream
+            return b
+        p = helpers.params(self.W, self.H, self.spp, self.bounces, use_ao=self.use_ao, ao=self.ao,
+                           seed=self.seed, compat=self.compat, chunks=self.chunks)
+        return b, p
+
+
+def _random_philox(seed):
+    return _random(seed)
+
+
+PHILOX_CASES = [
+    PhiloxCase("c2_queue", helpers.cornell, what="C2 scene, spp_chunks AUTO (queue kernel, QB -2)"),
+    PhiloxCase("c2_fixed_grid", helpers.cornell, chunks=1, what="C2 scene, fill_canva's order (fixed grid)"),
+    PhiloxCase("c2_ao_2p5", helpers.cornell, use_ao=True, ao=2.5, compat=0, chunks=4,
+               what="README box + AO 2.5 (double), queue kernel"),
+    PhiloxCase("glass_spheres", _glass, chunks=4, what="translucent spheres (QB -1)"),
+    PhiloxCase("hole_spheres_ao", _holes, use_ao=True, ao=2.0, chunks=3, what="alpha-hole spheres + AO"),
+    PhiloxCase("c3_pyramid", helpers.pyramid_scene, what="C3 scene, queue kernel (QB 0)"),
+    PhiloxCase("c3_pyramid_fixed", helpers.pyramid_scene, chunks=1, what="C3 scene, fixed grid"),
+    PhiloxCase("mineways", helpers.mineways_scene, chunks=4, what="alpha-hole texels, BVH queue kernel (QB 3)"),
+    PhiloxCase("c4_tree_ao", helpers.tree_scene, W=48, H=36, spp=8, bounces=8, use_ao=True, ao=2.5,
+               chunks=4, what="C4 scene (AO 2.5 -> 2, ThreadData's int), deep-tree opaque kernel"),
+    PhiloxCase("c4_tree_ao_2p5", helpers.tree_scene, W=40, H=30, spp=8, bounces=8, use_ao=True, ao=2.5,
+               compat=0, chunks=1, what="C4 scene with AO 2.5 as a double, fixed-grid BVH kernel"),
+] + [PhiloxCase("random_%d" % s, _random_philox(s), what="enclosed tests/test_gpu_fuzz.random_scene(%d)" % s)
+     for s in range(100, 116)]
+
+PHILOX_BY_NAME = {c.name: c for c in PHILOX_CASES}
+
+
+def plane_sha(a):
+    """sha256 of a plane's float64 bytes with NaN and -0.0 made canonical
+    (payloads and zero signs are not compared: gfx950 and x86 make
+    different default NaNs, and the parity suite compares with ==)."""
+    import hashlib
+    a = np.ascontiguousarray(a, dtype="<f8").copy()
+    a[np.isnan(a)] = np.nan
+    a[a == 0] = 0.0
+    return hashlib.sha256(a.tobytes()).hexdigest()

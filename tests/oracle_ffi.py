@@ -17,6 +17,7 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
 REF_SO = os.path.join(ORACLE_DIR, "_ref", "libref_leaf.so")
 REF_TRACER_SO = os.path.join(ORACLE_DIR, "_ref", "libref_tracer.so")
+REF_TRACER_PHILOX_SO = os.path.join(ORACLE_DIR, "_ref", "libref_tracer_philox.so")
 
 
 class OracleHit(C.Structure):
@@ -27,6 +28,7 @@ class OracleHit(C.Structure):
 _oracle = None
 _ref = None
 _ref_tracer = None
+_ref_tracer_philox = None
 
 
 def build_oracle():
@@ -154,6 +156,29 @@ def ref_tracer():
         lib.ref_tracer_srand.argtypes = [C.c_uint]
         _ref_tracer = lib
     return _ref_tracer
+
+
+def ref_tracer_philox():
+    """main.c:22-284 + denoiser.h:11-29 compiled verbatim with the GPU's
+    stream spec in place of glibc rand() / libm (oracle/ref_tracer_stream.h),
+    or None when /root/reference was absent."""
+    global _ref_tracer_philox
+    if _ref_tracer_philox is None:
+        if not os.path.exists(REF_TRACER_PHILOX_SO):
+            if os.path.exists("/root/reference/main.c"):
+                build_oracle()
+            if not os.path.exists(REF_TRACER_PHILOX_SO):
+                return None
+        lib = C.CDLL(REF_TRACER_PHILOX_SO)
+        P = C.POINTER
+        lib.ref_trace_rows_philox.argtypes = [P(Sphere), C.c_int, P(Triangle), C.c_int, P(Material), C.c_int,
+                                              C.c_int, P(C.c_int), P(Camera), C.c_int, C.c_int, C.c_int, C.c_int,
+                                              C.c_double, C.c_double, C.c_double, C.c_int, C.c_double,
+                                              C.c_ulonglong, C.c_int, C.c_int, C.c_int,
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        lib.ref_trace_rows_philox.restype = C.c_int
+        _ref_tracer_philox = lib
+    return _ref_tracer_philox
 
 
 def counters():
