@@ -30,7 +30,7 @@ extern "C" {
  *    spp_chunks to RT_SPP_CHUNKS_AUTO (a different summation grouping than
  *    the strict fill_canva order of spp_chunks = 1); build rt_params with
  *    rt_params_init so new fields read their defaults.  rt_gather_async.
- * 3: RT_CNT_BVH_STACK_OVER, RT_CNT_MBOX_SKIP appended (RT_NCOUNTERS 17 -> 19): d_counters
+ * 3: RT_CNT_BVH_STACK_OVER appended (RT_NCOUNTERS 17 -> 18): d_counters
  *    arrays of rt_count_async hold RT_NCOUNTERS entries; scenes above 65534
  *    spheres upload (exact sphere scans) instead of RT_EUNSUPPORTED.      */
 #define RT_ABI_VERSION 3
@@ -350,11 +350,6 @@ enum {
                              tree by its exact stack bound (rt_bvh.cpp); a
                              nonzero count means that bound is wrong (GPU
                              diagnostic, rt_count_async only)            */
-    RT_CNT_MBOX_SKIP,     /* brute-force casts whose wave skipped the
-                             triangle scan: no ray of the wave can meet
-                             the mesh box (GPU diagnostic, rt_count_async's
-                             fixed-grid waves; the scan's tests are still
-                             counted in RT_CNT_TRI_TESTS)                 */
     RT_NCOUNTERS
 };
 /* Same traversal as rt_render_async, no frame; adds event counts into the

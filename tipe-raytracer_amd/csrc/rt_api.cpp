@@ -153,9 +153,6 @@ struct rt_device_scene {
     int bvh_nodes = 0, bvh_depth = 0, bvh_stack4 = 0;
     double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0;
     float bvh_rbox = 0.0f;           // >= every |bound| of the BVH's boxes
-    bool mbox_ok = false;            // brute-force scenes: mbox / s_rel / s_abs / r_scene hold rt_bvh.h mesh_box
-    float mbox[6] = {0, 0, 0, 0, 0, 0};
-    float mbox_r = 0.0f;
     bool mats_bounded = false;       // every diffuse/emission/strength finite, |x| <= 2^100
     bool mats_bounded_f32 = false;   // ... |x| <= 2^50: RT_PREC_FP32's em = emis * es * 1.5 * AO stays < FLT_MAX
     bool sph_opaque = false;         // every sphere material takes main.c's opaque branch (no hole, no refraction)
@@ -354,16 +351,6 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.zero_exit = g_zero_exit.load() && p->semantics != RT_SEM_CUDA && sc->mats_bounded &&
                    (p->precision != RT_PREC_FP32 || sc->mats_bounded_f32) &&
                    (!kp.useAO || (AO > 0.0 && AO <= 1000.0 && std::fmax(sc->coord_max, cam) <= 0x1p20));
-    // brute-force scenes: the mesh-box pre-test (rt_bvh.h mesh_box) under the
-    // same origin bound as the BVH's padding
-    if (RT_MESH_BOX && !sc->bvh && sc->mbox_ok && p->accel == RT_ACCEL_AUTO && p->semantics != RT_SEM_CUDA &&
-        cam <= sc->r_scene) {
-        kp.mbox_on = 1;
-        for (int i = 0; i < 6; ++i) kp.mbox[i] = sc->mbox[i];
-        kp.mbox_r = sc->mbox_r;
-        kp.bvh_srel = sc->s_rel;
-        kp.bvh_sabs = sc->s_abs;
-    }
     if (sc->bvh && p->accel == RT_ACCEL_AUTO && cam <= sc->r_scene) {
         kp.bvh = sc->bvh;
         kp.bvhh = sc->bvhh;
@@ -783,18 +770,17 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     // triangle arrays are then stored in leaf order.  r_scene bounds every
     // coordinate a ray origin can take on the scene's surfaces.
     BvhBuild bvh;
-    double r_tri = 1.0;                      // bound on every coordinate a ray origin can take
-    for (int i = 0; i < scene->nbSpheres; ++i) {
-        const rt_sphere& q = scene->sphere_list[i];
-        for (int a = 0; a < 3; ++a) r_tri = std::max(r_tri, std::fabs(q.center.e[a]) + std::fabs(q.radius));
-    }
-    for (int i = 0; i < scene->nbTriangles; ++i) {
-        const rt_triangle& t = scene->triangle_list[i];
-        for (int a = 0; a < 3; ++a)
-            r_tri = std::max({r_tri, std::fabs(t.A.e[a]), std::fabs(t.B.e[a]), std::fabs(t.C.e[a])});
-    }
     if (scene->nbTriangles > 32) {           // (a BVH over C3's 5 triangles: 5118 -> 4482 Msamples/s)
-        const double r = r_tri;
+        double r = 1.0;
+        for (int i = 0; i < scene->nbSpheres; ++i) {
+            const rt_sphere& q = scene->sphere_list[i];
+            for (int a = 0; a < 3; ++a) r = std::max(r, std::fabs(q.center.e[a]) + std::fabs(q.radius));
+        }
+        for (int i = 0; i < scene->nbTriangles; ++i) {
+            const rt_triangle& t = scene->triangle_list[i];
+            for (int a = 0; a < 3; ++a)
+                r = std::max({r, std::fabs(t.A.e[a]), std::fabs(t.B.e[a]), std::fabs(t.C.e[a])});
+        }
         if (std::isfinite(r) && build_bvh(tri.data(), scene->nbTriangles, r, bvh)) {
             std::vector<TriGeo> tri2(tri.size());
             std::vector<TriTex> tex2(tex.size());
@@ -864,18 +850,6 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->s_rel = bvh.s_rel;
     ds->s_abs = bvh.s_abs;
     ds->r_scene = bvh.r_scene;
-    if (bvh.nodes4.empty() && scene->nbTriangles > 0 && std::isfinite(r_tri)) {
-        double srel = 0.0, sabs = 0.0;
-        if (mesh_box(tri.data(), scene->nbTriangles, r_tri, ds->mbox, ds->mbox + 3, srel, sabs)) {
-            float rb = 0.0f;
-            for (int i = 0; i < 6; ++i) rb = std::max(rb, std::fabs(ds->mbox[i]));
-            ds->mbox_r = rb * (1.0f + 0x1p-20f);
-            ds->mbox_ok = std::isfinite(ds->mbox_r);
-            ds->s_rel = srel;
-            ds->s_abs = sabs;
-            ds->r_scene = r_tri;
-        }
-    }
     {
         float rb = 0.0f;             // the single-precision slab margin's coordinate bound
         for (const BvhNode4& nd : bvh.nodes4)

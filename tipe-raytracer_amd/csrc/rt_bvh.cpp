@@ -162,28 +162,6 @@ struct Builder {
 
 double norm3(double x, double y, double z) { return std::sqrt(x * x + y * y + z * z); }
 
-// Triangle g's box grown by the header's delta_k (plus 2^-50 relative): every
-// ray-plane point of an accepted hit_triangle lies inside it.
-Box padded_box(const TriGeo& g, double r_scene)
-{
-    const double e1 = norm3(g.abx, g.aby, g.abz), e2 = norm3(g.acx, g.acy, g.acz);
-    const double delta = (e1 + e2) * (std::ldexp(1e6, -44) * ((e1 + e2) * 4.0 * r_scene + 6.0 * e1 * e2) +
-                                      std::ldexp(1.0, -48)) +
-                         std::ldexp(r_scene, -48);
-    const double A[3] = {g.ax, g.ay, g.az};
-    const double B[3] = {g.ax + g.abx, g.ay + g.aby, g.az + g.abz};
-    const double C[3] = {g.ax + g.acx, g.ay + g.acy, g.az + g.acz};
-    Box b;
-    b.grow(A);
-    b.grow(B);
-    b.grow(C);
-    for (int a = 0; a < 3; ++a) {
-        b.lo[a] -= delta + std::fabs(b.lo[a]) * std::ldexp(1.0, -50);
-        b.hi[a] += delta + std::fabs(b.hi[a]) * std::ldexp(1.0, -50);
-    }
-    return b;
-}
-
 // Collapse of the binary tree into 4-wide nodes: a node's children are its
 // binary children, with the internal child of largest box area replaced by
 // its own two children while fewer than four.  Boxes are copied (already
@@ -255,10 +233,23 @@ bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
     std::vector<Prim> P((size_t)nt);
     for (int i = 0; i < nt; ++i) {
         const TriGeo& g = tri[i];
+        const double e1 = norm3(g.abx, g.aby, g.abz), e2 = norm3(g.acx, g.acy, g.acz);
         maxN = std::max(maxN, norm3(g.nx, g.ny, g.nz));
+        const double delta = (e1 + e2) * (std::ldexp(1e6, -44) * ((e1 + e2) * 4.0 * r_scene + 6.0 * e1 * e2) +
+                                          std::ldexp(1.0, -48)) +
+                             std::ldexp(r_scene, -48);
+        const double A[3] = {g.ax, g.ay, g.az};
+        const double B[3] = {g.ax + g.abx, g.ay + g.aby, g.az + g.abz};
+        const double C[3] = {g.ax + g.acx, g.ay + g.acy, g.az + g.acz};
         Prim& p = P[(size_t)i];
-        p.box = padded_box(g, r_scene);
-        for (int a = 0; a < 3; ++a) p.c[a] = 0.5 * (p.box.lo[a] + p.box.hi[a]);
+        p.box.grow(A);
+        p.box.grow(B);
+        p.box.grow(C);
+        for (int a = 0; a < 3; ++a) {
+            p.box.lo[a] -= delta + std::fabs(p.box.lo[a]) * std::ldexp(1.0, -50);
+            p.box.hi[a] += delta + std::fabs(p.box.hi[a]) * std::ldexp(1.0, -50);
+            p.c[a] = 0.5 * (p.box.lo[a] + p.box.hi[a]);
+        }
         p.idx = i;
     }
     Builder bld{P, out.nodes};
@@ -320,27 +311,6 @@ bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
     out.s_abs = k * r_scene + std::ldexp(r_scene, -48);
     out.r_scene = r_scene;
     return true;
-}
-
-bool mesh_box(const TriGeo* tri, int nt, double r_scene, float lo[3], float hi[3], double& s_rel, double& s_abs)
-{
-    if (nt < 1 || !std::isfinite(r_scene)) return false;
-    Box u;
-    double maxN = 0.0;
-    for (int i = 0; i < nt; ++i) {
-        u.grow(padded_box(tri[i], r_scene));
-        maxN = std::max(maxN, norm3(tri[i].nx, tri[i].ny, tri[i].nz));
-    }
-    for (int a = 0; a < 3; ++a) {
-        if (!std::isfinite(u.lo[a]) || !std::isfinite(u.hi[a])) return false;
-        lo[a] = down(u.lo[a]);
-        hi[a] = up(u.hi[a]);
-        if (!std::isfinite(lo[a]) || !std::isfinite(hi[a])) return false;
-    }
-    const double k = std::ldexp(1e6, -44) * maxN;           // build_bvh's distance-cull slack
-    s_rel = k + std::ldexp(1.0, -48);
-    s_abs = k * r_scene + std::ldexp(r_scene, -48);
-    return std::isfinite(s_rel) && std::isfinite(s_abs);
 }
 
 // ---- 64-byte nodes (BvhNodeH) ------------------------------------------------

@@ -75,11 +75,4 @@ struct BvhBuild {
 // triangles or too many nodes) -> brute-force scan.
 bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out);
 
-// The brute-force scan's pre-test (scenes without a BVH): the union of the
-// triangles' padded boxes (build_bvh's per-triangle padding) rounded outward
-// to float, and build_bvh's distance-cull slack.  A ray that misses this box,
-// leaves it behind its origin or enters it beyond best*(1+s_rel)+s_abs can
-// neither hit nor tie any of the triangles.  false: non-finite values.
-bool mesh_box(const TriGeo* tri, int nt, double r_scene, float lo[3], float hi[3], double& s_rel, double& s_abs);
-
 }  // namespace rt

@@ -65,10 +65,6 @@ enum : int {
     U_COUNT
 };
 
-#ifndef RT_MESH_BOX                 // brute-force scenes: wave-uniform mesh-box pre-test (A/B knob)
-#define RT_MESH_BOX 0
-#endif
-
 // Everything one render launch needs, passed by value as the kernel argument.
 struct KParams {
     // scene
@@ -134,9 +130,6 @@ struct KParams {
     int ns_cand;             // spheres the candidate pass scans: ns_pad, or 0 when cand_lmax is +inf (every
                              // ray then takes the exact scan: non-finite spheres, or more than 65534
                              // spheres, whose slots do not fit RT_CAND_TAG's 16 bits)
-    int mbox_on;             // brute-force scenes (no BVH): the wave skips the triangle scan when no
-    float mbox[6];           // lane's ray can meet the mesh box mbox (lo xyz, hi xyz; rt_bvh.h mesh_box,
-    float mbox_r;            // culled with bvh_srel / bvh_sabs) -- mbox_r >= every |bound|
 };
 
 struct UniBlock { double v[U_COUNT]; };

@@ -931,23 +931,6 @@ __device__ __forceinline__ int cast_spheres(const KParams& kp, const V3 o, const
     return win;
 }
 
-// The brute-force scan's pre-test (RT_MESH_BOX): box4's conservative
-// single-precision slab test on the mesh box (host: rt_bvh.h mesh_box, the
-// triangles' padded boxes), with the BVH's distance cull.  false: no triangle
-// can hit or tie for this ray (its scan would find nothing).
-__device__ __forceinline__ bool mesh_box_hit(const KParams& kp, const V3 o, const V3 d, double best)
-{
-    const Ray32 r = ray32(o, d, kp.mbox_r);
-    const float nsabs = (float)(-kp.bvh_sabs) * (1.0f + 0x1p-22f);
-    const bool sx = __float_as_uint(r.ix) >> 31, sy = __float_as_uint(r.iy) >> 31, sz = __float_as_uint(r.iz) >> 31;
-    const float px = sx ? kp.mbox[3] : kp.mbox[0], qx = sx ? kp.mbox[0] : kp.mbox[3];
-    const float py = sy ? kp.mbox[4] : kp.mbox[1], qy = sy ? kp.mbox[1] : kp.mbox[4];
-    const float pz = sz ? kp.mbox[5] : kp.mbox[2], qz = sz ? kp.mbox[2] : kp.mbox[5];
-    const float tmin = fmaxf(fmaxf(fmaf(px, r.ix, r.ax), fmaf(py, r.iy, r.ay)), fmaf(pz, r.iz, r.az));
-    const float tmax = fminf(fminf(fmaf(qx, r.ix, r.bx), fmaf(qy, r.iy, r.by)), fmaf(qz, r.iz, r.bz));
-    return fmaxf(tmin, nsabs) <= fminf(tmax, cull32(kp, best));
-}
-
 template <bool COUNT, bool BVH, bool CU = false, bool AMGM = false>
 __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const V3 d, double& t_best, int& idx,
                                            Cnt& cnt)
@@ -961,12 +944,8 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
     } else if (BVH) {
         tris_bvh<COUNT, CU>(kp, o, d, best, kind, win, win_orig, cnt);
     } else if (RT_TRI_BF && !COUNT && !kp.tri_orig) {
-        // the wave skips the scan when none of its rays can meet the mesh box
-        if (!RT_MESH_BOX || !kp.mbox_on || __ballot(mesh_box_hit(kp, o, d, best)) != 0ull)
-            for (int k = 0; k < kp.nt; ++k) tri_test_bf<CU>(kp, k, o, d, best, kind, win);
+        for (int k = 0; k < kp.nt; ++k) tri_test_bf<CU>(kp, k, o, d, best, kind, win);
     } else {
-        if (COUNT && RT_MESH_BOX && kp.mbox_on && __ballot(mesh_box_hit(kp, o, d, best)) == 0ull)
-            cnt.c[RT_CNT_MBOX_SKIP] += 1;
         for (int k = 0; k < kp.nt; ++k) tri_test<COUNT, CU, false, true>(kp, k, o, d, best, kind, win, win_orig);
     }
     t_best = best;

@@ -39,11 +39,11 @@ def rt_chunk_bound(c, S, P):
  RT_CNT_TRI_TESTS, RT_CNT_SHADE, RT_CNT_TEX_HITS, RT_CNT_REFRACT,
  RT_CNT_RNG_DRAWS, RT_CNT_EXACT_RESCANS, RT_CNT_BVH_NODES, RT_CNT_BVH_TRI_TESTS,
  RT_CNT_BVH_LANE_SLOTS, RT_CNT_LEAF_LANE_SLOTS, RT_CNT_CAST_LANE_SLOTS, RT_CNT_SHADE_LANE_SLOTS,
- RT_CNT_BVH_STACK_OVER, RT_CNT_MBOX_SKIP, RT_NCOUNTERS) = range(19)
+ RT_CNT_BVH_STACK_OVER, RT_NCOUNTERS) = range(18)
 COUNTER_NAMES = ["samples", "casts", "sphere_tests", "sphere_disc", "tri_tests",
                  "shade", "tex_hits", "refract", "rng_draws", "exact_rescans",
                  "bvh_nodes", "bvh_tri_tests", "bvh_lane_slots", "leaf_lane_slots", "cast_lane_slots",
-                 "shade_lane_slots", "bvh_stack_over", "mbox_skip"]
+                 "shade_lane_slots", "bvh_stack_over"]
 RT_ACCEL_AUTO, RT_ACCEL_NONE = 0, 1
 RT_SKY_OFF, RT_SKY_LAST_SPHERE = 0, 1
 RT_SEM_MAIN_C, RT_SEM_CUDA = 0, 1

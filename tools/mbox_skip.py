@@ -1,6 +1,8 @@
 """Fraction of brute-force casts whose wave skips the triangle scan (rt.h
 RT_CNT_MBOX_SKIP, RT_MESH_BOX pre-test) on C3 / C5, from rt_count_async at a
-few spp.  Usage: python tools/mbox_skip.py"""
+few spp.  Usage: python tools/mbox_skip.py
+Needs the library of commit 8bc63d2 (the RT_MESH_BOX experiment, measured
+C3 -3.1 % / C5 -2.9 % and removed again; profiles/r05_mbox/)."""
 import json
 import os
 import sys
