@@ -229,6 +229,11 @@ bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
     out = BvhBuild();
     if (const char* e = std::getenv("RT_BVH_LEAF")) kLeaf = std::max(1, std::min(16, std::atoi(e)));
     if (nt <= kLeaf) return false;
+    // The SAH build makes leaves of kLeaf triangles except where the depth cap
+    // binds, so a mesh of more than 65535 * kLeaf triangles gets >= 65535
+    // internal nodes, which the uint16 traversal stack entries refuse (checked
+    // again below): refuse before paying for the sweep build.
+    if ((nt + kLeaf - 1) / kLeaf - 1 >= 65535) return false;
     double maxN = 0.0;
     std::vector<Prim> P((size_t)nt);
     for (int i = 0; i < nt; ++i) {

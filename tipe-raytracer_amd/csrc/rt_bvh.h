@@ -7,7 +7,9 @@
 
 namespace rt {
 
-constexpr int kMaxDepth = 30;       // the kernel's LDS stack holds kMaxDepth + 1 entries
+constexpr int kMaxDepth = 30;       // binary build depth cap (leaves below it hold several triangles); the
+                                    // kernels admit a tree by its exact stack bound (BvhBuild::stack4 vs
+                                    // kStack4 / kStackQ / kStackQ4), not by its depth
 
 // One internal node: the padded boxes of both children (one 64-byte fetch
 // per visit).  Bounds are the padded double boxes rounded OUTWARD to float

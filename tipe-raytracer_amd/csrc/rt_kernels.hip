@@ -629,9 +629,11 @@ __device__ __forceinline__ unsigned short* bvh_stack()
 // The queue kernel's per-lane stack (BVH scenes): [kStackQ][256] uint16, 12 KiB,
 // which keeps the kernel at 4 blocks (16 waves) per CU; trees that could need
 // more entries (kp.bvh_stack > kStackQ) render with the fixed-grid kernel.
-// The QB = 4 instantiation serves shallow trees only (depth4 <= 4: at most 13
-// entries) and keeps 14, so its top-node cache and the task table fit the
-// same 40 KiB.
+// The QB = 4 instantiation (shallow trees: bvh_steps 4, i.e. depth4 <= 4) is
+// admitted only when the tree's exact stack bound (rt_bvh.cpp stack4) is at
+// most kStackQ4 = 14 entries, so its top-node cache and the task table fit the
+// same 40 KiB; deeper or wider trees take QB = 3 (kStackQ) or the fixed grid
+// (stack_cap_of below; RT_CNT_BVH_STACK_OVER checks the bound on the GPU).
 constexpr int kStackQ = 24, kStackQ4 = 14;
 // The LDS stack entries of the kernel launch_render picks for a tree: the
 // queue kernel's QB = 4 (kStackQ4) or QB = 3 (kStackQ) instantiation, else
