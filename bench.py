@@ -262,59 +262,6 @@ def configs_extra(dev, stream, cam):
     return out
 
 
-def fp32_extra(dev, stream, cam, spheres):
-    """rt_params.precision = RT_PREC_FP32 (not bit-exact): kernel rates of C2
-    (1000 spp, the headline frame) and C4 (64 spp) beside north_star's parity
-    gate, the per-channel RMSE of pre-gamma radiance and of canva/255 against
-    the fp64 frame of the same seeds (which the parity suite pins bit for bit
-    to the oracle) -- never `value`."""
-    out = {}
-    sptr = stream.cuda_stream
-    cases = {"C2": (tipe_rt.make_scene(spheres), 1000, 6, False), "C4": (config_scene("tree")[0], 64, 8, True)}
-    for name, (sc, spp, bounces, ao) in cases.items():
-        w, h = 1200, 900
-        ds = tipe_rt.DeviceScene(sc, dev.index)
-        tiling = tipe_rt.band_tiling(0, h - 1)
-        frames = {}
-        ms = None
-        for prec in (tipe_rt.types.RT_PREC_FP64, tipe_rt.types.RT_PREC_FP32):
-            p = tipe_rt.make_params(w, h, spp, bounces, cam, focus=3.0, use_ao=ao, ao=2.5, seed=SEED,
-                                    chunks=tipe_rt.RT_SPP_CHUNKS_AUTO, precision=prec)
-            buf = torch.empty((4, h, w, 3), dtype=torch.float64, device=dev)
-
-            def launch():
-                tipe_rt.render_async(ds, p, tiling, buf[0].data_ptr(), buf[1].data_ptr(), buf[2].data_ptr(),
-                                     buf[3].data_ptr(), sptr)
-            launch()
-            torch.cuda.synchronize(dev)
-            frames[prec] = buf
-            if prec == tipe_rt.types.RT_PREC_FP32:
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-                ev[0].record(stream)
-                for _ in range(2):
-                    launch()
-                ev[1].record(stream)
-                torch.cuda.synchronize(dev)
-                ms = ev[0].elapsed_time(ev[1]) / 2
-        ds.close()
-        f64, f32 = frames[tipe_rt.types.RT_PREC_FP64], frames[tipe_rt.types.RT_PREC_FP32]
-
-        def rmse(a, b):
-            d = (a - b).reshape(-1, 3)
-            return [round(float(x), 7) for x in torch.sqrt((d * d).mean(0)).cpu()]
-        rad = rmse(torch.nan_to_num(f32[3]), torch.nan_to_num(f64[3]))
-        can = rmse(f32[0] / 255.0, f64[0] / 255.0)
-        out[name] = {"kernel_msamples_per_s": round(w * h * spp / (ms * 1e-3) / 1e6, 1), "spp_measured": spp,
-                     "kernel_ms": round(ms, 3), "dtype": "f32",
-                     "rmse_radiance_per_channel": rad, "rmse_canva_over_255_per_channel": can,
-                     "nonfinite_mismatch": int((torch.isfinite(f32[3]) != torch.isfinite(f64[3])).sum()),
-                     "meets_north_star_1e-4": bool(max(rad + can) <= 1e-4)}
-    out["note"] = ("RT_PREC_FP32: same integrator and draws in binary32, sums fp64; not bit-exact. RMSE vs the "
-                   "fp64 frame of the same seeds (bit-identical to the oracle by the parity suite); north_star "
-                   "gate 1e-4 per channel")
-    return out
-
-
 # ---- C3 / C4 / C5 row-tiled over the N ranks (N > 1) -------------------------
 def _max_over_ranks(x, dev, backend):
     t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
@@ -844,7 +791,6 @@ def main():
         if world == 1 and not args.no_extras:
             rec["configs"] = configs_extra(dev, stream, cam)
             rec["end_to_end"] = end_to_end(scene, spheres, cam)
-            rec["fp32_mode"] = fp32_extra(dev, stream, cam, spheres)
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(scene, cam, threads=args.cpu_threads)
             rec["speedup_vs_cpu_baseline"] = round(value / rec["cpu_baseline"]["value"], 1)

@@ -123,16 +123,13 @@ typedef struct rt_params {
  * closest_hit is commented out, main.c:64-71).  LAST_SPHERE enables that
  * branch: when the last sphere is the closest hit, its emissionColor becomes
  * the sky texel sphere_uvmapping (texture.h:92-112) picks and its alpha 1. */
-/* rt_params.precision.  FP64 (default) is the reference's arithmetic, in its
- * operation order: images equal the CPU oracle's bit for bit.  FP32 is
- * EXPERIMENTAL (measured 1.1-3.4e-4 per-channel RMSE against the oracle's
- * FP64 frames, above north_star's 1e-4; frozen, never the benchmark): it runs the
- * same integrator (main.c semantics, same Philox draws and draw order) in
- * binary32 -- ray/sphere (stable roots), ray/triangle, sampler, shading --
- * with the per-pixel sums and the resolve kept in fp64.  It is NOT bit-exact:
- * paths whose float decisions differ diverge.  The GPU tests bound its
- * difference from FP64 (tests/test_fp32_mode.py).  FP32 needs
- * RT_SEM_MAIN_C; it runs the fixed-grid kernel. */
+/* rt_params.precision.  FP64 (default and only renderable value) is the
+ * reference's arithmetic in its operation order: images equal the reference's
+ * own compiled composition bit for bit (tests/test_gpu_reference.py).
+ * RT_PREC_FP32 (an experimental binary32 integrator, r02-r04) was removed in
+ * r05: its measured 1.1-3.4e-4 per-channel RMSE against the FP64 frames was
+ * above north_star's 1e-4.  It is rejected with RT_EUNSUPPORTED; the value
+ * stays reserved so the struct keeps its meaning. */
 #define RT_PREC_FP64 0
 #define RT_PREC_FP32 1
 
@@ -236,10 +233,9 @@ void* rt_fill_canva(void* thread_data);
  * Process-wide; returns the previous setting. */
 int rt_set_fill_spp_chunks(int spp_chunks);
 
-/* The rt_params.precision rt_fill_canva renders with: RT_PREC_FP64 (default,
- * bit-exact) or RT_PREC_FP32 (the fast mode, not bit-exact; see
- * rt_params.precision).  Other values select FP64.  Process-wide; returns the
- * previous setting. */
+/* The rt_params.precision rt_fill_canva renders with.  Since r05 always
+ * RT_PREC_FP64 (RT_PREC_FP32 was removed, see rt_params.precision): any
+ * argument selects FP64.  Process-wide; returns the previous setting. */
 int rt_set_fill_precision(int precision);
 
 /* rt_render_rows / rt_fill_canva keep the uploaded scene (and its BVH) of

@@ -105,10 +105,10 @@ int validate_params(const rt_params* p)
         return fail(RT_EINVAL, "unknown semantics %d", p->semantics);
     if (p->semantics == RT_SEM_CUDA && p->sky_mode != RT_SKY_OFF)
         return fail(RT_EINVAL, "sky_mode needs RT_SEM_MAIN_C (main_cuda.cu has no sky)");
-    if (p->precision != RT_PREC_FP64 && p->precision != RT_PREC_FP32)
-        return fail(RT_EINVAL, "unknown precision %d", p->precision);
-    if (p->precision == RT_PREC_FP32 && p->semantics != RT_SEM_MAIN_C)
-        return fail(RT_EUNSUPPORTED, "RT_PREC_FP32 needs RT_SEM_MAIN_C");
+    if (p->precision == RT_PREC_FP32)
+        return fail(RT_EUNSUPPORTED, "RT_PREC_FP32 was removed (r05): its 1.1-3.4e-4 per-channel RMSE against the "
+                                     "reference exceeded north_star's 1e-4; only the bit-exact FP64 path renders");
+    if (p->precision != RT_PREC_FP64) return fail(RT_EINVAL, "unknown precision %d", p->precision);
     if ((unsigned long long)p->largeur_image * (unsigned long long)p->hauteur_image > 0xffffffffull)
         return fail(RT_EUNSUPPORTED, "pixel index exceeds the 32-bit Philox counter word");
     return RT_OK;
@@ -154,7 +154,6 @@ struct rt_device_scene {
     double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0;
     float bvh_rbox = 0.0f;           // >= every |bound| of the BVH's boxes
     bool mats_bounded = false;       // every diffuse/emission/strength finite, |x| <= 2^100
-    bool mats_bounded_f32 = false;   // ... |x| <= 2^50: RT_PREC_FP32's em = emis * es * 1.5 * AO stays < FLT_MAX
     bool sph_opaque = false;         // every sphere material takes main.c's opaque branch (no hole, no refraction)
     bool tri_opaque = false;         // ... every texel too, and no triangle uses material index 3 or 4
     double coord_max = HUGE_VAL;     // max |coordinate| of the spheres (|C_a| + R) and triangle vertices
@@ -278,7 +277,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.sph_disp = sc->sph_disp;
     kp.tri_mat = sc->tri_mat;
     kp.cuda = p->semantics == RT_SEM_CUDA ? 1 : 0;
-    kp.f32 = p->precision == RT_PREC_FP32 ? 1 : 0;
+    kp.f32 = 0;                      // (RT_PREC_FP32 removed in r05; the field keeps the kernarg layout)
     for (int i = 0; i < 6; ++i) kp.cbb[i] = sc->cbb[i];
     if (p->sky_mode == RT_SKY_LAST_SPHERE && sc->sky && sc->ns > 0) {
         kp.sky = sc->sky;
@@ -345,11 +344,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     cam += 0.5 * (std::fabs(ox) + std::fabs(oy));
     // Zero-throughput exit (rt_kernels.hip LanePath::zero_rc): exact when the
     // shading values are bounded and, with AO, the AO factor stays finite.
-    // RT_PREC_FP32 forms em = emis * es * 1.5 * AO in binary32: with every
-    // shading value within 2^50 (and AO <= 1000) it stays below FLT_MAX, so a
-    // zero rayColor still makes every later bounce add exactly 0.
     kp.zero_exit = g_zero_exit.load() && p->semantics != RT_SEM_CUDA && sc->mats_bounded &&
-                   (p->precision != RT_PREC_FP32 || sc->mats_bounded_f32) &&
                    (!kp.useAO || (AO > 0.0 && AO <= 1000.0 && std::fmax(sc->coord_max, cam) <= 0x1p20));
     if (sc->bvh && p->accel == RT_ACCEL_AUTO && cam <= sc->r_scene) {
         kp.bvh = sc->bvh;
@@ -660,9 +655,9 @@ const char* rt_last_render_kernel(void) { return last_render_kernel(); }
 
 const char* rt_version(void)
 {
-    return "tipe-raytracer-mi355x 0.4 (abi 2, gfx950; precision FP64 bit-exact by default; RT_PREC_FP32 is "
-           "EXPERIMENTAL: not bit-exact and above north_star's 1e-4 per-channel RMSE (1.1-3.4e-4); "
-           "rt_params_init defaults spp_chunks to RT_SPP_CHUNKS_AUTO, a fixed per-pixel slice grouping)";
+    return "tipe-raytracer-mi355x 0.5 (abi 3, gfx950; precision FP64, bit-exact against the reference's own "
+           "composition; RT_PREC_FP32 removed (RT_EUNSUPPORTED); rt_params_init defaults spp_chunks to "
+           "RT_SPP_CHUNKS_AUTO, a fixed per-pixel slice grouping)";
 }
 
 int rt_device_count(void)
@@ -803,12 +798,11 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         for (long long i = 0; i < n_texels; ++i) texels[(size_t)i] = to_dev(scene->mat_list[i]);
     }
 
-    bool mats_bounded = true, mats_bounded_f32 = true;
+    bool mats_bounded = true;
     double coord_max = 0.0;
     for (const std::vector<DevMat>* v : {&sph_mat, &texels, &sky})
         for (const DevMat& m : *v) {
             mats_bounded = mats_bounded && shading_bounded(m);
-            mats_bounded_f32 = mats_bounded_f32 && shading_bounded(m, 0x1p50);
         }
     for (int i = 0; i < scene->nbSpheres; ++i) {
         const rt_sphere& q = scene->sphere_list[i];
@@ -824,7 +818,6 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     rt_device_scene* ds = new rt_device_scene();
     ds->device = device;
     ds->mats_bounded = mats_bounded;
-    ds->mats_bounded_f32 = mats_bounded_f32;
     const auto opaque_mat = [](const DevMat& m) { return !(m.alpha < 0.0001) && !(m.alpha <= 0.99); };
     ds->sph_opaque = std::all_of(sph_mat.begin(), sph_mat.end(), opaque_mat);
     // tri_material (rt_kernels.hip): the texel's alpha, overridden for
@@ -957,8 +950,6 @@ int rt_count_async(const rt_device_scene* scene, const rt_params* params, const 
     int rc;
     if ((rc = validate_params(params)) || (rc = validate_tiling(tiling))) return rc;
     if (!d_counters) return fail(RT_EINVAL, "d_counters is NULL");
-    if (params->precision == RT_PREC_FP32)     // the counters instrument the fp64 integrator only
-        return fail(RT_EUNSUPPORTED, "rt_count_async counts the fp64 integrator; precision FP32 has no COUNT build");
     KParams kp;
     double uni[U_COUNT];
     make_kparams(scene, params, tiling, kp, uni);
@@ -1370,8 +1361,8 @@ int rt_set_fill_spp_chunks(int spp_chunks)
 }
 int rt_set_fill_precision(int precision)
 {
-    if (precision != RT_PREC_FP32) precision = RT_PREC_FP64;
-    return g_fill_prec.exchange(precision);
+    (void)precision;                 // RT_PREC_FP32 was removed (r05): rt_fill_canva renders FP64
+    return g_fill_prec.exchange(RT_PREC_FP64);
 }
 int rt_scene_cache_clear(void) { return scene_cache_clear(); }
 rt_denoise_fn rt_get_denoise_hook(void) { return g_denoise.load(); }

@@ -82,7 +82,7 @@ struct KParams {
     const DevMat* sky;       // sky texels when sky mode is on, else null
     const DevMat* tri_mat;   // rt_triangle.mat per triangle (leaf order with a BVH): RT_SEM_CUDA
     int cuda;                // rt.h RT_SEM_CUDA (render_kernel_cuda)
-    int f32;                 // rt.h RT_PREC_FP32 (render_kernel_f32)
+    int f32;                 // always 0: RT_PREC_FP32 was removed in r05 (field kept: kernarg layout)
     double cbb[6];           // RT_SEM_CUDA: the triangles' box (lo xyz, hi xyz), hit_BBox
     const double* sph_rinv;  // 1/radius per sphere (sphere_uvmapping's divide)
     const double* sph_disp;  // per sphere: hsl round trip of its emission (main.c:155-158), 3 doubles

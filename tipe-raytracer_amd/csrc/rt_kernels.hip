@@ -9,7 +9,7 @@
 //   fill_canva        main.c:245-284      -> render_kernel_q (task queue) /
 //                                            render_kernel (fixed grid), combine_kernel
 //   tracer            main.c:118-242      -> QPath (queue kernel), LanePath
-//                                            (fixed grid), samples_f32 (FP32 mode)
+//                                            (fixed grid)
 //   closest_hit       main.c:52-92        -> closest_hit()
 //   ambient_occlusion main.c:94-116       -> ao_factor()
 //   hit_sphere        sphere.h:13-47      -> sphere_exact() (+ candidate pass)
@@ -1904,428 +1904,6 @@ __device__ __forceinline__ void render_body(const KParams& kp)
     }
 }
 
-// ---- RT_PREC_FP32 (rt.h): the integrator in binary32 ----------------------
-// tracer (main.c:118-242) with closest_hit (main.c:52-92), hit_sphere
-// (sphere.h:13-47), hit_triangle (mesh.h:70-94), random_dir_no_norm
-// (rtutility.h:189-203), refracted_vec (rtutility.h:210-227) and
-// ambient_occlusion (main.c:94-116) evaluated in float: the same draws in the
-// same order (Philox stream, rt.h), the same branches and thresholds, but
-// binary32 rounding, so NOT bit-exact -- a path whose float decision differs
-// from the fp64 one diverges.  Sphere roots use the stable form (q = -(h +
-// sign(h) sqrt(D)), roots q/a and c/q) since the radius-500 walls cancel in
-// the textbook form, and c comes from k = |C|^2 - r^2.  Materials, textures, the sky texel and the emitter
-// display are looked up as in fp64 (their inputs rounded once); per-pixel sums
-// and the resolve stay fp64.  Spheres (<= kF32Sph) and brute-force triangles
-// (<= kF32Tri) are staged in LDS as floats once per block; BVH scenes walk the
-// same 4-wide tree with the single-precision slab test (box4).
-struct F3 {
-    float x, y, z;
-};
-__device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
-__device__ __forceinline__ F3 f3v(V3 v) { return F3{(float)v.x, (float)v.y, (float)v.z}; }
-__device__ __forceinline__ V3 v3f(F3 v) { return v3((double)v.x, (double)v.y, (double)v.z); }
-__device__ __forceinline__ F3 add3(F3 a, F3 b) { return F3{a.x + b.x, a.y + b.y, a.z + b.z}; }
-__device__ __forceinline__ F3 sub3(F3 a, F3 b) { return F3{a.x - b.x, a.y - b.y, a.z - b.z}; }
-__device__ __forceinline__ F3 mul3(F3 a, float s) { return F3{a.x * s, a.y * s, a.z * s}; }
-__device__ __forceinline__ F3 mulv3(F3 a, F3 b) { return F3{a.x * b.x, a.y * b.y, a.z * b.z}; }
-__device__ __forceinline__ float dot3(F3 a, F3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
-__device__ __forceinline__ F3 cross3(F3 a, F3 b)
-{
-    return F3{fmaf(a.y, b.z, -a.z * b.y), fmaf(a.z, b.x, -a.x * b.z), fmaf(a.x, b.y, -a.y * b.x)};
-}
-__device__ __forceinline__ F3 norm3(F3 v)
-{
-    const float l2 = dot3(v, v);
-    return l2 > 0.0f ? mul3(v, __builtin_amdgcn_rsqf(l2)) : v;
-}
-__device__ __forceinline__ float unit31f(uint32_t r) { return (float)r * 0x1p-31f; }
-
-constexpr int kF32Sph = 256;         // spheres staged in LDS (float4: centre, |C|^2 - r^2)
-constexpr int kF32Tri = 32;          // brute-force triangles staged in LDS (4 float4: A, AB, AC, N)
-
-struct F32Scene {
-    const float4* sph;   // LDS copy, or null (then kp.sph, converted per test)
-    const float4* tri;   // LDS copy (brute force), or null
-};
-
-__device__ __forceinline__ float4 f32_sphere(const KParams& kp, const F32Scene& fs, int k)
-{
-    if (fs.sph) return fs.sph[k];
-    const SphCand s = kp.sph_cand[k];
-    return make_float4((float)s.cx, (float)s.cy, (float)s.cz, (float)s.k);
-}
-
-// hit_sphere in float (thresholds of sphere.h:28-41: t1 >= 1e-4, else t2 >=
-// 1e-4).  c = |o - C|^2 - r^2 is formed as |o|^2 - 2 o.C + k with k = |C|^2 -
-// r^2 from the host (SphCand, long double): for the radius-500 walls the
-// textbook |o - C|^2 - r^2 rounds at ulp(2.5e5) and leaves hit points ~3e-5
-// off the surface (grazing bounce rays then re-hit the wall they leave);
-// this form rounds at ulp(1e3), ~1e-7 off.
-__device__ __forceinline__ int spheres_f32(const KParams& kp, const F32Scene& fs, F3 o, F3 d, float& best)
-{
-    const float a = dot3(d, d), ia = __builtin_amdgcn_rcpf(a);
-    const float od = dot3(o, d), oo = dot3(o, o);
-    const F3 m2o = mul3(o, -2.0f);
-    int win = -1;
-    for (int k = 0; k < kp.ns; ++k) {
-        const float4 s = f32_sphere(kp, fs, k);
-        const float h = od - fmaf(s.z, d.z, fmaf(s.y, d.y, s.x * d.x));
-        const float c = fmaf(m2o.z, s.z, fmaf(m2o.y, s.y, fmaf(m2o.x, s.x, s.w))) + oo;
-        const float D = fmaf(h, h, -a * c);
-        if (D > 0.0f) {
-            const float q = -(h + copysignf(__builtin_sqrtf(D), h));
-            const float r1 = q * ia, r2 = c * __builtin_amdgcn_rcpf(q);
-            const float t1 = fminf(r1, r2), t2 = fmaxf(r1, r2);
-            const float t = t1 >= 0.0001f ? t1 : t2;
-            if (t >= 0.0001f && t < best) {
-                best = t;
-                win = k;
-            }
-        }
-    }
-    return win;
-}
-
-// hit_triangle in float (mesh.h:70-94: det >= 1e-6, dst/u/v/w >= 1e-7), with
-// the fp64 path's (dst, caller index) tie-break
-__device__ __forceinline__ void tri_f32(const KParams& kp, const F32Scene& fs, int k, F3 o, F3 d, float& best,
-                                        int& kind, int& win, int& win_orig)
-{
-    F3 A, AB, AC, N;
-    if (fs.tri) {
-        const float4 r0 = fs.tri[4 * k], r1 = fs.tri[4 * k + 1], r2 = fs.tri[4 * k + 2], r3 = fs.tri[4 * k + 3];
-        A = f3(r0.x, r0.y, r0.z);
-        AB = f3(r1.x, r1.y, r1.z);
-        AC = f3(r2.x, r2.y, r2.z);
-        N = f3(r3.x, r3.y, r3.z);
-    } else {
-        const TriGeo g = kp.tri[k];
-        A = f3((float)g.ax, (float)g.ay, (float)g.az);
-        AB = f3((float)g.abx, (float)g.aby, (float)g.abz);
-        AC = f3((float)g.acx, (float)g.acy, (float)g.acz);
-        N = f3((float)g.nx, (float)g.ny, (float)g.nz);
-    }
-    const float det = -dot3(d, N);
-    if (det >= 1E-6f) {
-        const F3 ao = sub3(o, A);
-        const F3 dao = cross3(ao, d);
-        const float inv = 1.0f / det;
-        const float dst = dot3(ao, N) * inv;
-        if (dst >= 1E-7f && dst <= best) {
-            const int orig = kp.tri_orig ? kp.tri_orig[k] : k;
-            if (dst < best || (kind == HIT_TRI && orig < win_orig)) {
-                const float u = dot3(AC, dao) * inv;
-                const float v = -dot3(AB, dao) * inv;
-                const float w = 1.0f - u - v;
-                if (u >= 1E-7f && v >= 1E-7f && w >= 1E-7f) {
-                    best = dst;
-                    kind = HIT_TRI;
-                    win = k;
-                    win_orig = orig;
-                }
-            }
-        }
-    }
-}
-
-// closest_hit in float: spheres, then the triangles (BVH walk or brute force)
-template <bool BVH>
-__device__ __forceinline__ int closest_f32(const KParams& kp, const F32Scene& fs, F3 o, F3 d, float& t, int& idx)
-{
-    float best = __builtin_huge_valf();
-    int win = spheres_f32(kp, fs, o, d, best);
-    int kind = win >= 0 ? HIT_SPHERE : HIT_NONE, win_orig = 0;
-    if (BVH) {
-        // bvh_step's walk with the float triangle test; box4's slab test is
-        // already single precision (conservative on the padded boxes)
-        unsigned short* stk = bvh_stack();
-        const Ray32 r32 = ray32(v3f(o), v3f(d), kp.bvh_rbox);
-        int node = 0, sp = 0;
-        while (true) {
-            const BvhNode4* nd = kp.bvh + node;
-            bool h[4];
-            float tn[4];
-            int Ch[4], Cn[4];
-            box4(kp, nd, r32, cull32(kp, (double)best), h, tn, Ch, Cn);
-            int next = -1;
-            float tnext = 0.0f;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                if (!h[c]) continue;
-                const int ch = nd->child[c], n = nd->count[c];
-                if (n > 0) {
-                    for (int k = ch; k < ch + n; ++k) tri_f32(kp, fs, k, o, d, best, kind, win, win_orig);
-                } else if (next < 0) {
-                    next = ch;
-                    tnext = tn[c];
-                } else {
-                    int push = ch;
-                    if (tn[c] < tnext) {
-                        push = next;
-                        next = ch;
-                        tnext = tn[c];
-                    }
-                    if (sp < kStack4) stk[sp++ * 256] = (unsigned short)push;
-                }
-            }
-            if (next >= 0) {
-                node = next;
-                continue;
-            }
-            if (sp == 0) break;
-            node = stk[--sp * 256];
-        }
-    } else {
-        for (int k = 0; k < kp.nt; ++k) tri_f32(kp, fs, k, o, d, best, kind, win, win_orig);
-    }
-    t = best;
-    idx = win;
-    return kind;
-}
-
-// random_dir_no_norm + its normalize (rtutility.h:189-203) in float:
-// cos(phi) = 2v - 1 and sin(phi) = sqrt(1 - cos^2) for phi = acos(2v - 1)
-__device__ __forceinline__ F3 random_dir_f32(Stream& st)
-{
-    const float u = unit31f(st.next31()), v = unit31f(st.next31());
-    const float th = 6.28318530717958647692f * u;
-    const float cp = fmaf(2.0f, v, -1.0f);
-    const float sp = __builtin_sqrtf(fmaxf(0.0f, fmaf(-cp, cp, 1.0f)));
-    float sn, cs;
-    __sincosf(th, &sn, &cs);
-    return norm3(f3(cs * sp, sn * sp, cp));
-}
-
-__device__ __forceinline__ F3 refracted_f32(F3 v, F3 nrm, float n1, float n2)
-{
-    n1 *= n1;                                    // rtutility.h:214-215 (squared indices, reference quirk)
-    n2 *= n2;
-    const float r = n1 / n2;
-    const float cn = dot3(nrm, v);
-    const float radical = 1.0f - (r * r) * (1.0f - cn * cn);
-    if (radical > 0.0f)
-        return add3(mul3(sub3(v, mul3(nrm, cn)), r), mul3(f3(-nrm.x, -nrm.y, -nrm.z), __builtin_sqrtf(radical)));
-    return sub3(v, mul3(nrm, 2.0f * cn));
-}
-
-template <bool BVH>
-__device__ __forceinline__ float ao_f32(const KParams& kp, const F32Scene& fs, F3 p, F3 n, float AO, Stream& st)
-{
-    const F3 dir = norm3(add3(n, random_dir_f32(st)));
-    float t;
-    int idx;
-    float occ = 0.0f;
-    if (closest_f32<BVH>(kp, fs, p, dir, t, idx) != HIT_NONE) {
-        const F3 df = mul3(dir, t);                  // hitPoint - point
-        const float att = __builtin_sqrtf(dot3(df, df)) / t;
-        occ = powf(att, AO);
-    }
-    return occ / AO;
-}
-
-// The samples [s0, s1) of one pixel as a flat loop of bounces (tracer,
-// main.c:118-242, in float): one iteration is one bounce of the sample in
-// flight, and a lane whose path ends starts its next sample's camera ray in
-// the next iteration, so a wave does not wait for its longest path before
-// any lane moves on (the fp64 kernels' LanePath rounds, in miniature).
-template <bool BVH, bool SKY>
-__device__ __forceinline__ void samples_f32(const KParams& kp, const F32Scene& fs, int x, int g, uint32_t pixel,
-                                            int s0, int s1, uint32_t* rng, double* acc)
-{
-    if (kp.B <= 0) return;                               // tracer adds (0, 0, 0) everywhere
-    Stream st;
-    F3 o, d, inc, rc;
-    bool chain = true;
-    float top_n2 = 1.0f;
-    int i = 0, s = s0;
-    st.start(pixel, 0u, kp.key0, kp.key1, rng);          // the keys stay wave-uniform (SGPRs)
-    auto start = [&]() {                                 // the camera ray of sample s (main.c:258-270)
-        st.sample = (uint32_t)(kp.s_base + s);
-        st.n = 0;
-        V3 no, rd;
-        camera_ray<false>(kp, x, g, st, no, rd);
-        o = f3v(no);
-        d = f3v(rd);
-        inc = f3(0, 0, 0);
-        rc = f3(1, 1, 1);
-        chain = true;
-        top_n2 = 1.0f;
-        i = 0;
-    };
-    if (s < s1) start();
-    while (s < s1) {
-        bool end = false, add_inc = true;
-        float t;
-        int idx;
-        const int kind = closest_f32<BVH>(kp, fs, o, d, t, idx);
-        if (kind == HIT_NONE) {                          // miss: the path ends, main.c:236-238
-            if (chain) {
-                acc_add(acc, ACC_ALB, v3(0, 0, 0));
-                acc_add(acc, ACC_NRM, v3(0, 0, 0));
-            }
-            end = true;
-        } else {
-            const F3 hp = add3(o, mul3(d, t));
-            F3 hn;
-            Mat mat;
-            if (kind == HIT_SPHERE) {
-                const float4 sg = f32_sphere(kp, fs, idx);
-                hn = norm3(sub3(hp, f3(sg.x, sg.y, sg.z)));
-                mat = load_mat(kp.sph_mat + idx);
-                if (SKY && idx == kp.ns - 1) sky_material(kp, idx, kp.sph[idx], v3f(hp), mat);
-            } else {
-                const TriGeo tg = kp.tri[idx];
-                const V3 hn64 = normalize(v3(tg.nx, tg.ny, tg.nz));
-                hn = f3v(hn64);
-                mat = tri_material(kp, idx, v3f(hp), hn64);
-            }
-            const float alpha = (float)mat.alpha;
-            bool lit = false;
-            if (chain) {
-                if (mat.es > 0) {                        // direct view of a light, main.c:154-160
-                    V3 col;
-                    if (kind == HIT_SPHERE && !(SKY && idx == kp.ns - 1)) {
-                        const double* sd = kp.sph_disp + 3 * idx;
-                        col = v3(sd[0], sd[1], sd[2]);
-                    } else {
-                        col = hsl_roundtrip(mat.emis);
-                    }
-                    acc_add(acc, ACC_RAD, col);
-                    acc_add(acc, ACC_ALB, col);
-                    acc_add(acc, ACC_NRM, v3f(hn));
-                    lit = true;
-                } else if (!(alpha < 0.0001f) || i == kp.B - 1) {
-                    acc_add(acc, ACC_ALB, mat.diff);
-                    acc_add(acc, ACC_NRM, v3f(hn));
-                    chain = alpha < 0.0001f;
-                }
-            }
-            if (lit) {
-                end = true;
-                add_inc = false;
-            } else {
-                o = hp;
-                const F3 diffuse_dir = norm3(add3(hn, random_dir_f32(st)));
-                const F3 reflected_dir = sub3(d, mul3(hn, 2.0f * dot3(d, hn)));
-                const F3 dr = add3(diffuse_dir, mul3(sub3(reflected_dir, diffuse_dir), (float)mat.rs));
-                bool shaded = !(alpha < 0.0001f);            // alpha hole: pass through, main.c:200-206
-                if (shaded) {
-                    chain = false;
-                    if (alpha <= 0.99f) {                    // refraction, main.c:167-193
-                        F3 nn = hn;
-                        float n1, n2;
-                        const float ior = (float)mat.ior;
-                        if (dot3(d, hn) > 0.0f) {
-                            nn = f3(-hn.x, -hn.y, -hn.z);
-                            n1 = ior;
-                            n2 = top_n2;
-                        } else {
-                            n1 = top_n2;
-                            n2 = ior;
-                            top_n2 = ior;
-                        }
-                        const F3 refr = refracted_f32(d, nn, n1, n2);
-                        if (unit31f(st.next31()) > alpha) {
-                            d = refr;
-                            shaded = false;
-                        }
-                    }
-                }
-                if (shaded) {
-                    d = dr;
-                    const F3 diff = f3v(mat.diff), emis = f3v(mat.emis);
-                    if (kp.useAO) {
-                        const float AO = (float)((cdptr)kp.uni)[opq0() + U_AO];
-                        inc = add3(inc, mulv3(mul3(emis, (float)mat.es * 1.5f * AO), rc));
-                        if (rc.x > 0.5f || rc.y > 0.5f || rc.z > 0.5f) rc = mulv3(diff, mul3(rc, 1.3f));
-                        rc = mulv3(diff, rc);
-                        rc = mul3(rc, ao_f32<BVH>(kp, fs, hp, hn, AO, st));
-                    } else {
-                        inc = add3(inc, mulv3(mul3(emis, (float)mat.es), rc));
-                        if (rc.x > 0.5f || rc.y > 0.5f || rc.z > 0.5f) rc = mulv3(diff, mul3(rc, 1.3f));
-                        rc = mulv3(diff, rc);
-                    }
-                    // zero-throughput exit (host-gated as for fp64, LanePath::zero_rc):
-                    // the chain is over and every later bounce adds emis * 0
-                    if (kp.zero_exit && rc.x == 0.0f && rc.y == 0.0f && rc.z == 0.0f) end = true;
-                }                                            // (a hole's ray goes on unchanged)
-                ++i;
-                if (i >= kp.B) end = true;
-            }
-        }
-        if (end) {
-            if (add_inc) acc_add(acc, ACC_RAD, v3f(inc));
-            ++s;
-            if (s < s1) start();
-        }
-    }
-}
-
-// fill_canva's thread = (pixel, chunk of its samples), as render_body, with
-// samples_f32.  The camera ray is built in fp64 (camera_ray) and rounded.
-template <bool BVH, bool SKY>
-__global__ __launch_bounds__(256) void render_kernel_f32(const KParams kp)
-{
-    __shared__ double acc_lds[9 * 256];
-    __shared__ uint32_t rng_lds[4 * 256];
-    __shared__ float4 sph_lds[kF32Sph];
-    __shared__ float4 tri_lds[BVH ? 1 : 4 * kF32Tri];
-    F32Scene fs{nullptr, nullptr};
-    if (kp.ns <= kF32Sph) {
-        for (int k = threadIdx.x; k < kp.ns; k += 256) {
-            const SphCand s = kp.sph_cand[k];
-            sph_lds[k] = make_float4((float)s.cx, (float)s.cy, (float)s.cz, (float)s.k);
-        }
-        fs.sph = sph_lds;
-    }
-    if (!BVH && kp.nt <= kF32Tri) {
-        for (int k = threadIdx.x; k < kp.nt; k += 256) {
-            const TriGeo g = kp.tri[k];
-            tri_lds[4 * k] = make_float4((float)g.ax, (float)g.ay, (float)g.az, 0.0f);
-            tri_lds[4 * k + 1] = make_float4((float)g.abx, (float)g.aby, (float)g.abz, 0.0f);
-            tri_lds[4 * k + 2] = make_float4((float)g.acx, (float)g.acy, (float)g.acz, 0.0f);
-            tri_lds[4 * k + 3] = make_float4((float)g.nx, (float)g.ny, (float)g.nz, 0.0f);
-        }
-        fs.tri = tri_lds;
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int ly = kp.band_y0 + blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const int chunk = blockIdx.z;
-    bool valid = x < kp.W && ly < kp.local_rows && ly < kp.band_y0 + kp.band_rows;
-    int g = 0;
-    if (valid) {
-        const int lt = ly / kp.tile_rows, yy = ly - lt * kp.tile_rows;
-        g = kp.row_base + (kp.tile_first + lt * kp.tile_step) * kp.tile_rows + yy;
-        valid = g < kp.row_end;
-    }
-    if (!valid) return;
-    const uint32_t pixel = (uint32_t)g * (uint32_t)kp.W + (uint32_t)x;
-    const int s0 = chunk_start(kp.S, kp.chunks, kp.chunk_taper, kp.chunk_den, 0u, (unsigned)chunk);
-    const int s1 = chunk_start(kp.S, kp.chunks, kp.chunk_taper, kp.chunk_den, 0u, (unsigned)chunk + 1u);
-    double* acc = acc_lds + threadIdx.x;
-    const long long li = (long long)ly * kp.W + x;
-    const bool carry = kp.sums && kp.chunks == 1;
-#pragma unroll
-    for (int j = 0; j < 9; ++j) acc[j * 256] = carry ? kp.sums[li * 9 + j] : 0.0;
-    samples_f32<BVH, SKY>(kp, fs, x, g, pixel, s0, s1, rng_lds + threadIdx.x, acc);
-    const V3 srad = v3(acc[0], acc[256], acc[512]);
-    const V3 salb = v3(acc[768], acc[1024], acc[1280]);
-    const V3 snrm = v3(acc[1536], acc[1792], acc[2048]);
-    if (carry) {
-#pragma unroll
-        for (int j = 0; j < 9; ++j) kp.sums[li * 9 + j] = acc[j * 256];
-    } else if (kp.chunks == 1) {
-        write_pixel(kp, li, srad, salb, snrm);
-    } else {
-        double* p = kp.partial + ((long long)chunk * kp.band_rows * kp.W + ((long long)(ly - kp.band_y0) * kp.W + x)) * 9;
-        p[0] = srad.x; p[1] = srad.y; p[2] = srad.z;
-        p[3] = salb.x; p[4] = salb.y; p[5] = salb.z;
-        p[6] = snrm.x; p[7] = snrm.y; p[8] = snrm.z;
-    }
-}
-
 // fill_canva, main.c:245-284: thread = (pixel, chunk of its samples).
 template <bool COUNT, bool BVH, bool SKY>
 __global__ __launch_bounds__(256, BVH ? RT_WAVES_PER_SIMD_BVH : RT_WAVES_PER_SIMD) void render_kernel(const KParams kp)
@@ -3225,12 +2803,7 @@ static void launch_variant(const KParams& kp_in, void* stream)
     const dim3 g = grid_for(kp_in);
     const hipStream_t st = (hipStream_t)stream;
     KParams kp = kp_in;
-    if (!COUNT && kp.f32) {
-        if (kp.bvh && kp.sky) hipLaunchKernelGGL((render_kernel_f32<true, true>), g, dim3(256), 0, st, kp);
-        else if (kp.bvh) hipLaunchKernelGGL((render_kernel_f32<true, false>), g, dim3(256), 0, st, kp);
-        else if (kp.sky) hipLaunchKernelGGL((render_kernel_f32<false, true>), g, dim3(256), 0, st, kp);
-        else hipLaunchKernelGGL((render_kernel_f32<false, false>), g, dim3(256), 0, st, kp);
-    } else if (kp.cuda && kp.bvh) hipLaunchKernelGGL((render_kernel_cuda<COUNT, true>), g, dim3(256), 0, st, kp);
+    if (kp.cuda && kp.bvh) hipLaunchKernelGGL((render_kernel_cuda<COUNT, true>), g, dim3(256), 0, st, kp);
     else if (kp.cuda) hipLaunchKernelGGL((render_kernel_cuda<COUNT, false>), g, dim3(256), 0, st, kp);
     else if (kp.bvh && kp.sky) hipLaunchKernelGGL((render_kernel<COUNT, true, true>), g, dim3(256), 0, st, kp);
     else if (kp.bvh) hipLaunchKernelGGL((render_kernel<COUNT, true, false>), g, dim3(256), 0, st, kp);
@@ -3314,7 +2887,7 @@ int launch_render(const KParams& kp, void* stream)
         qb = stack_cap_of(kp.bvh_stack, kp.bvh_steps) == kStackQ ? 3 : 4;
         qbvh = qb == 4 || !RT_QNODE_H || kp.bvhh != nullptr;
     }
-    if (kp.task_ctr && kp.chunks > 1 && (!kp.bvh || qbvh) && !kp.cuda && !kp.f32 && !kp.sums) {
+    if (kp.task_ctr && kp.chunks > 1 && (!kp.bvh || qbvh) && !kp.cuda && !kp.sums) {
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
@@ -3359,7 +2932,7 @@ int launch_render(const KParams& kp, void* stream)
 #endif
     {
         launch_variant<false>(kp, stream);
-        t_last_kernel = kp.f32 ? "render_kernel_f32" : kp.cuda ? "render_kernel_cuda" : kp.bvh ? "render_kernel<BVH>"
+        t_last_kernel = kp.cuda ? "render_kernel_cuda" : kp.bvh ? "render_kernel<BVH>"
                                                                                                  : "render_kernel";
     }
     if (kp.chunks > 1) {
