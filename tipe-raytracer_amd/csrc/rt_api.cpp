@@ -794,6 +794,8 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     long long n_texels = 0;
     if (scene->nbTriangles > 0) {
         n_texels = (long long)scene->nbMaterials * scene->tex_width * scene->tex_height;
+        if (n_texels >= (1LL << 31))     // the kernels index texels in 32 bits (160 GiB of texels)
+            return fail(RT_EUNSUPPORTED, "%lld texels >= 2^31", n_texels);
         texels.resize((size_t)n_texels);
         for (long long i = 0; i < n_texels; ++i) texels[(size_t)i] = to_dev(scene->mat_list[i]);
     }

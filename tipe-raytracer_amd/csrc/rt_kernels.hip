@@ -955,8 +955,16 @@ __device__ __forceinline__ int closest_hit(const KParams& kp, const V3 o, const 
     return kind;
 }
 
-// tri_uvmapping + get_barycentric_coord, texture.h:16-27,44-90.
-__device__ __forceinline__ Mat tri_material(const KParams& kp, int k, const V3 P, const V3 n)
+// tri_uvmapping + get_barycentric_coord, texture.h:16-27,44-90, in two
+// steps: the texel a hit picks (barycentrics, uv, fmod, the clamped index)
+// and the material read from it (with the material-index overrides).  A
+// refraction lane keeps the TexRef from resolve_hit to finish_bounce instead
+// of recomputing the barycentrics (host: n_texels < 2^31).
+struct TexRef {
+    int index;                        // clamped texel index
+    int m;                            // the triangle's material index (quelMatPourTri)
+};
+__device__ __forceinline__ TexRef tri_texel(const KParams& kp, int k, const V3 P, const V3 n)
 {
     const TriGeo g = kp.tri[k];
     const TriTex tx = kp.tri_tex[k];
@@ -979,7 +987,12 @@ __device__ __forceinline__ Mat tri_material(const KParams& kp, int k, const V3 P
     long long index = ((long long)y * kp.tw + x) + ((long long)kp.th * kp.tw * m);
     index = index < 0 ? 0 : index;                       // reference UB -> clamp
     index = index >= kp.n_texels ? kp.n_texels - 1 : index;
-    Mat res = load_mat(kp.texels + index);
+    return TexRef{(int)index, m};
+}
+__device__ __forceinline__ Mat texel_material(const KParams& kp, TexRef t)
+{
+    const int m = t.m;
+    Mat res = load_mat(kp.texels + t.index);
     const cdptr b = kcb();
     if (m == 1) {
         res.emis = v3(1, 1, 1);
@@ -997,6 +1010,10 @@ __device__ __forceinline__ Mat tri_material(const KParams& kp, int k, const V3 P
         res.rs = KCV(b, KC_RS3);          // 0.3
     }
     return res;
+}
+__device__ __forceinline__ Mat tri_material(const KParams& kp, int k, const V3 P, const V3 n)
+{
+    return texel_material(kp, tri_texel(kp, k, P, n));
 }
 
 // Sky branch of closest_hit (main.c:64-71, commented out in the reference;
@@ -1978,6 +1995,8 @@ struct QHit {
     V3 hn;                           // the hit's normal
     double rs;                       // its reflectionStrength
     bool refr, hole;                 // refraction decided after the direction draws; alpha hole
+    TexRef tex;                      // (triangle hits) the texel resolve_hit read: the refraction branch
+                                     // re-reads the material from it instead of redoing the barycentrics
 };
 
 // NT: the scene has no triangles (every hit is a sphere); OP: every material
@@ -1985,7 +2004,11 @@ struct QHit {
 // and no refraction branch is ever taken and neither is compiled in)
 // IR: incomingLight / rayColor live in the lane's LDS column (slots
 // ACC_SLOTS..+5 of the sums array) instead of twelve VGPRs
-template <bool SKY, int AOM, bool NT = false, bool OP = false, int IR = 0>   // IR 1: incomingLight only
+// KT: a refraction lane keeps its triangle hit's texel (QHit::tex) from
+// resolve_hit to finish_bounce instead of redoing the barycentrics (the
+// brute-force kernel, QB 0: C3 +7.0 %, C5 +6.7 %; the BVH kernels recompute,
+// their registers are tighter: sweep -1.9 % with KT)
+template <bool SKY, int AOM, bool NT = false, bool OP = false, int IR = 0, bool KT = false>   // IR 1: incomingLight only
 struct QPath {
     V3 o, d, cd, inc, rc;            // cd: the cast's direction (AO casts; else d)
     double* accp;                    // (IR) the lane's LDS column
@@ -2028,16 +2051,29 @@ struct QPath {
         }
     }
 
-    // The hit's material (tri_material / sky_material are pure functions of
-    // the hit, so a refraction lane recomputes it instead of keeping it live).
-    __device__ __forceinline__ Mat hit_material(const KParams& kp, V3 hp, V3 hn) const
+    // The hit's material (sky_material / texel_material are pure functions of
+    // the hit, so a refraction lane re-reads it instead of keeping it live;
+    // for a triangle it keeps only the texel, H.tex).
+    __device__ __forceinline__ Mat hit_material(const KParams& kp, V3 hp, QHit& H) const
     {
         if (NT || kind == HIT_SPHERE) {
             Mat mat = load_mat(kp.sph_mat + win);
             if (SKY && win == kp.ns - 1) sky_material(kp, win, kp.sph[win], hp, mat);
             return mat;
         }
-        return tri_material(kp, win, hp, hn);
+        if (!KT) return tri_material(kp, win, hp, H.hn);
+        H.tex = tri_texel(kp, win, hp, H.hn);
+        return texel_material(kp, H.tex);
+    }
+    __device__ __forceinline__ Mat hit_material_again(const KParams& kp, V3 hp, const QHit& H) const
+    {
+        if (NT || kind == HIT_SPHERE) {
+            Mat mat = load_mat(kp.sph_mat + win);
+            if (SKY && win == kp.ns - 1) sky_material(kp, win, kp.sph[win], hp, mat);
+            return mat;
+        }
+        if (!KT) return tri_material(kp, win, hp, H.hn);
+        return texel_material(kp, H.tex);
     }
 
     __device__ __forceinline__ static bool zero_rc_of(const KParams& kp, V3 r)
@@ -2104,7 +2140,7 @@ struct QPath {
                 const TriGeo tg = kp.tri[win];
                 H.hn = normalize(v3(tg.nx, tg.ny, tg.nz));
             }
-            const Mat mat = hit_material(kp, hp, H.hn);
+            const Mat mat = hit_material(kp, hp, H);
             bool lit = false;
             if (chain) {
                 if (mat.es > 0) {                        // direct view of a light, main.c:154-160
@@ -2198,7 +2234,7 @@ struct QPath {
         const V3 dr = dn + muls(reflected_dir - dn, H.rs);
         bool shaded = true;
         if (!OP && H.refr) {                               // main.c:167-193
-            const Mat mat = hit_material(kp, o, H.hn);
+            const Mat mat = hit_material_again(kp, o, H);
             V3 nn = H.hn;
             double n1, n2;
             if (dot(d, H.hn) > 0) {                        // leaving: pop restores the stack
@@ -2284,7 +2320,7 @@ void render_kernel_q(const KParams kp)
     uint32_t* rng = rng_lds + threadIdx.x;
     const int lane = threadIdx.x & 63;
     unsigned qb = 0, qe = 0;         // the wave's batch of tasks [qb, qe) (wave-uniform)
-    QPath<SKY, AOM, QB < 0, QB == -2 || OPQ, QIR> L;
+    QPath<SKY, AOM, QB < 0, QB == -2 || OPQ, QIR, QB == 0> L;
     L.accp = acc;
     L.o = L.d = L.cd = L.inc = L.rc = v3(0, 0, 0);
     L.inc_set(v3(0, 0, 0));
