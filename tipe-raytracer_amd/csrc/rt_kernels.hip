@@ -114,12 +114,6 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
                                     // many lanes wait for it (samples_coop)
 #define RT_FLAT_FILL 2              // fixed-grid sphere kernel: camera rays start once this many eighths
                                     // of the live lanes wait (samples_flat)
-#ifndef RT_LEAF_PP                  // BVH queue kernel: a visit's single hit leaf waits in a register and the
-#define RT_LEAF_PP 0                // round's waiting leaves are tested together after its walk steps (A/B knob)
-#endif
-#ifndef RT_LEAF_PP_THR              // ... every round (0), or only for walks that are over and when at least
-#define RT_LEAF_PP_THR 0            // this many lanes have a leaf waiting
-#endif
 #ifndef RT_WALK_PRIO                // BVH queue kernel: wave priority during its walk steps (0: off).  The walk
 #define RT_WALK_PRIO 2              // is a chain of dependent node/record loads; ahead of the other waves'
 #endif                              // VALU it issues sooner: C4 +2.0..2.4 %, sweep +1.7..2.6 % (levels 1-3
@@ -821,11 +815,10 @@ __device__ __forceinline__ void box4h(const KParams& kp, const BvhNodeH* nd, uin
 // the next node (nearest hit internal child, else the stack top).  Returns
 // false when the traversal is over.  tris_bvh loops it to the end; the
 // resumable trace (render_sm) runs a bounded number of visits per round.
-template <bool COUNT, bool CU, int NTOP = 0, bool H = false, bool PP = false>
+template <bool COUNT, bool CU, int NTOP = 0, bool H = false>
 __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3 d, const Ray32& r32,
                                          unsigned short* stk, int& node, int& sp, double& best, int& kind,
-                                         int& win, int& win_orig, Cnt& cnt, const void* top = nullptr,
-                                         int* pt = nullptr)
+                                         int& win, int& win_orig, Cnt& cnt, const void* top = nullptr)
 {
     // NTOP > 0: the first NTOP nodes (breadth-first: the top levels) are read
     // from the block's LDS copy `top`, the rest from HBM/L2; H: 64-byte nodes
@@ -867,20 +860,6 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
                 stk[sp * 256] = (unsigned short)push;
                 ++sp;
             }
-        }
-    }
-    // PP: a lane whose visit hit exactly one leaf of one triangle and that
-    // has no leaf waiting yet keeps it in *pt instead of testing it now (the
-    // caller tests the waiting leaves after its walk steps; the winner is the
-    // (dst, caller index) minimum whatever the order, and a later test only
-    // culls less meanwhile).
-    if (PP && *pt < 0 && lm != 0u && (lm & (lm - 1u)) == 0u) {
-        const int c = __ffs(lm) - 1;
-        const int ch = c == 0 ? Ch[0] : c == 1 ? Ch[1] : c == 2 ? Ch[2] : Ch[3];
-        const int n = c == 0 ? Cn[0] : c == 1 ? Cn[1] : c == 2 ? Cn[2] : Cn[3];
-        if (n == 1) {
-            *pt = ch;
-            lm = 0u;
         }
     }
     // The triangles of every hit leaf in one loop, one triangle per lane and
@@ -2356,8 +2335,6 @@ void render_kernel_q(const KParams kp)
     L.state = SM_CAM;                // s = 0 >= s1 = 0: takes a task first
     int x = 0, g = 0, s1 = 0;
     int node = 0, sp = 0, win_orig = 0;      // BVH walk in flight (state SM_TRAV)
-    constexpr bool LPP = RT_LEAF_PP == 2 ? QB > 0 : (RT_LEAF_PP == 1 && QB == 3);
-    int pt = -1;                             // (LPP) the lane's waiting leaf triangle
     unsigned chunk = 0, p = 0, pixel = 0;
     bool owns = false;               // the lane's LDS sums belong to task (chunk, p)
     // sphere / brute-force scenes (QB 0): each wave decodes its batches of tasks into LDS
@@ -2413,19 +2390,11 @@ void render_kernel_q(const KParams kp)
                 for (int j = 0; j < QB; ++j) {
                     if (L.state == SM_TRAV) {
                         Cnt cnt;
-                        if (!bvh_step<false, false, NTOP, HN, LPP>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind,
-                                                                    L.win, win_orig, cnt, top, &pt))
+                        if (!bvh_step<false, false, NTOP, HN>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind, L.win,
+                                                           win_orig, cnt, top))
                             L.state = SM_RESOLVE;
                     }
                     if (__ballot(L.state == SM_TRAV) == 0ull) break;
-                }
-                // the waiting leaves, one test per lane: every round, or (RT_LEAF_PP_THR)
-                // when the walk is over or at least that many lanes have one waiting
-                const bool flush = RT_LEAF_PP_THR == 0 || L.state != SM_TRAV ||
-                                   __popcll(__ballot(pt >= 0)) >= RT_LEAF_PP_THR;
-                if (LPP && pt >= 0 && flush) {
-                    tri_test<false, false, true>(kp, pt, L.o, dd, L.best, L.kind, L.win, win_orig);
-                    pt = -1;
                 }
 #if RT_WALK_PRIO
                 __builtin_amdgcn_s_setprio(0);
