@@ -157,6 +157,7 @@ struct rt_device_scene {
     bool sph_opaque = false;         // every sphere material takes main.c's opaque branch (no hole, no refraction)
     bool tri_opaque = false;         // ... every texel too, and no triangle uses material index 3 or 4
     double coord_max = HUGE_VAL;     // max |coordinate| of the spheres (|C_a| + R) and triangle vertices
+    bool all_tex0 = false;           // every triangle's uv are 0: its texel is TriTex::tex0
 };
 
 namespace {
@@ -346,6 +347,11 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     // shading values are bounded and, with AO, the AO factor stays finite.
     kp.zero_exit = g_zero_exit.load() && p->semantics != RT_SEM_CUDA && sc->mats_bounded &&
                    (!kp.useAO || (AO > 0.0 && AO <= 1000.0 && std::fmax(sc->coord_max, cam) <= 0x1p20));
+    // TriTex::tex0 (constant texels of uv-less triangles): a hit point P is then
+    // within ~2^101 of the origin, the signed areas of get_barycentric_coord stay
+    // below 2^205 and areaABC >= |N| (1 - 2^-50) with |N| >= 1e-6 / |d| for any
+    // hit (det >= 1e-6), so the barycentrics are finite and u = v = +-0
+    kp.tex_const = sc->all_tex0 && std::fmax(sc->coord_max, cam) <= 0x1p100;
     if (sc->bvh && p->accel == RT_ACCEL_AUTO && cam <= sc->r_scene) {
         kp.bvh = sc->bvh;
         kp.bvhh = sc->bvhh;
@@ -758,7 +764,29 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         x.ucu = t.uvC.u;
         x.ucv = t.uvC.v;
         x.mat = scene->quelMatPourTri[i];
-        x.pad = 0;
+        x.tex0 = -1;
+        if (t.uvA.u == 0.0 && t.uvA.v == 0.0 && t.uvB.u == 0.0 && t.uvB.v == 0.0 && t.uvC.u == 0.0 &&
+            t.uvC.v == 0.0) {
+            // tri_uvmapping (texture.h:44-90) with every uv 0: u = v = +-0 for
+            // finite barycentrics, so x = y = 0 and the index is tw*th*mat (clamped
+            // into the table as the kernel clamps it)
+            const long long nt = (long long)scene->nbMaterials * scene->tex_width * scene->tex_height;
+            long long idx = (long long)scene->tex_height * scene->tex_width * x.mat;
+            idx = idx < 0 ? 0 : idx;
+            idx = idx >= nt ? nt - 1 : idx;
+            if (nt > 0 && nt < (1LL << 31)) x.tex0 = (int)idx;
+        }
+        // hit_triangle's normal, vec3_normalize(normalVect) (mesh.h:91, vec3.h:137-139):
+        // a pure function of the triangle, computed once here with the reference's
+        // operations (IEEE sqrt and divisions, no contraction) instead of per hit
+        const double nl = std::sqrt((g.nx * g.nx + g.ny * g.ny) + g.nz * g.nz);
+        x.unx = g.nx / nl;
+        x.uny = g.ny / nl;
+        x.unz = g.nz / nl;
+        // get_barycentric_coord's areaABC (texture.h:18) with the hit normal n = un:
+        // dot(n, cross(B - A, C - A)) = dot(un, N), constant per triangle
+        x.area = (x.unx * g.nx + x.uny * g.ny) + x.unz * g.nz;
+        x.rarea = 1.0 / x.area;
         tri_mat[i] = to_dev(t.mat);
     }
     // Triangle BVH (rt_bvh.cpp) over scenes with more than 32 triangles; the
@@ -829,6 +857,8 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     for (int i = 0; i < scene->nbTriangles && ds->tri_opaque; ++i)
         if (scene->quelMatPourTri[i] == 3 || scene->quelMatPourTri[i] == 4) ds->tri_opaque = false;
     ds->coord_max = coord_max;
+    ds->all_tex0 = scene->nbTriangles > 0 &&
+                   std::all_of(tex.begin(), tex.end(), [](const TriTex& x) { return x.tex0 >= 0; });
     ds->ns = scene->nbSpheres;
     ds->ns_pad = ns_pad;
     ds->cand_lmax = cand_lmax;

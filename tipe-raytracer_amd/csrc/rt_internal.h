@@ -10,7 +10,7 @@
 //                          (winner, fallback scan; r2 = -inf padding)
 //   DevMat  [ns]     80 B  sphere material — gathered for the winner only
 //   TriGeo  [nt]     96 B  A, B-A, C-A, N  — scanned wave-uniformly
-//   TriTex  [nt]    104 B  B, C, uvA/B/C, material — winner only
+//   TriTex  [nt]    144 B  B, C, uvA/B/C, material, unit normal, area terms — winner only
 //   BvhNode4[nodes] 128 B  four child boxes (rt_bvh.h) when nt > 32; the
 //   int     [nt]           triangle arrays are then in leaf order and
 //                          tri_orig maps back to the caller's order
@@ -49,13 +49,17 @@ struct TriTex {                                       // what tri_uvmapping read
     double bx, by, bz, cx, cy, cz;
     double uau, uav, ubu, ubv, ucu, ucv;
     int mat;                 // quelMatPourTri[i]
-    int pad;
+    int tex0;                // the texel index when every uv is 0 (it is then (0, 0) of
+                             // material mat for any finite hit), else -1
+    double unx, uny, unz;    // vec3_normalize(N) (mesh.h:91), host-computed: the hit normal
+    double area;             // get_barycentric_coord's areaABC = dot(un, N) (texture.h:18)
+    double rarea;            // 1 / area, correctly rounded (div_core's reciprocal)
 };
 static_assert(sizeof(SphGeo) == 32, "SphGeo");
 static_assert(sizeof(SphCand) == 32, "SphCand");
 static_assert(sizeof(DevMat) == 80, "DevMat");
 static_assert(sizeof(TriGeo) == 96, "TriGeo");
-static_assert(sizeof(TriTex) == 104, "TriTex");
+static_assert(sizeof(TriTex) == 144, "TriTex");
 
 // uniform block (doubles)
 enum : int {
@@ -99,6 +103,9 @@ struct KParams {
     int W, H, S, B;
     int useAO;
     int zero_exit;           // paths end once rayColor == 0 (host: only where exact, LanePath::zero_rc)
+    int tex_const;           // TriTex::tex0 stands for tri_texel (host: every triangle has one,
+                             // and every coordinate and ray origin is within 2^100, so the
+                             // barycentrics of a hit are finite)
     int cam_pin;             // aperture 0 and no -0 camera coordinate: co + (jx*0, jy*0, 0) == co exactly
     uint32_t key0, key1;
     int chunks;              // samples of a pixel split into this many chunks

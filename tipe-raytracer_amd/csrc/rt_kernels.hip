@@ -114,6 +114,15 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
                                     // many lanes wait for it (samples_coop)
 #define RT_FLAT_FILL 2              // fixed-grid sphere kernel: camera rays start once this many eighths
                                     // of the live lanes wait (samples_flat)
+#ifndef RT_TRI_UNORM                // triangle hits read the host-normalized normal (A/B knob)
+#define RT_TRI_UNORM 1
+#endif
+#ifndef RT_TEX_CONST                // uv-less triangles take their constant texel (TriTex::tex0; A/B knob)
+#define RT_TEX_CONST 1
+#endif
+#ifndef RT_TEX_RC                   // texel barycentrics divide on the host's 1/areaABC (A/B knob)
+#define RT_TEX_RC 0
+#endif
 #ifndef RT_WALK_PRIO                // BVH queue kernel: wave priority during its walk steps (0: off).  The walk
 #define RT_WALK_PRIO 2              // is a chain of dependent node/record loads; ahead of the other waves'
 #endif                              // VALU it issues sooner: C4 +2.0..2.4 %, sweep +1.7..2.6 % (levels 1-3
@@ -964,16 +973,43 @@ struct TexRef {
     int index;                        // clamped texel index
     int m;                            // the triangle's material index (quelMatPourTri)
 };
+// hit_triangle's normal vec3_normalize(N) (mesh.h:91): RT_TRI_UNORM reads the
+// host's copy (TriTex::un*, the same IEEE operations) instead of normalizing N
+// per hit
+__device__ __forceinline__ V3 tri_normal(const KParams& kp, int k)
+{
+    if (RT_TRI_UNORM) {
+        const TriTex* t = kp.tri_tex + k;
+        return v3(t->unx, t->uny, t->unz);
+    }
+    const TriGeo* g = kp.tri + k;
+    return normalize(v3(g->nx, g->ny, g->nz));
+}
 __device__ __forceinline__ TexRef tri_texel(const KParams& kp, int k, const V3 P, const V3 n)
 {
+    if (RT_TEX_CONST && kp.tex_const)            // every uv 0: the texel does not depend on P
+        return TexRef{kp.tri_tex[k].tex0, kp.tri_tex[k].mat};
     const TriGeo g = kp.tri[k];
     const TriTex tx = kp.tri_tex[k];
     const V3 A = v3(g.ax, g.ay, g.az), B = v3(tx.bx, tx.by, tx.bz), C = v3(tx.cx, tx.cy, tx.cz);
-    const double areaABC = dot(n, v3(g.nx, g.ny, g.nz));      // cross(B-A, C-A) == N
+    // areaABC = dot(n, cross(B-A, C-A)) = dot(n, N): n is the triangle's own
+    // unit normal (tri_normal), so the host's TriTex::area is the same value
+    const double areaABC = RT_TRI_UNORM ? tx.area : dot(n, v3(g.nx, g.ny, g.nz));
     const double areaPBC = dot(n, cross(B - P, C - P));
     const double areaPCA = dot(n, cross(C - P, A - P));
-    const double b0 = areaPBC / areaABC;
-    const double b1 = areaPCA / areaABC;
+    double b0, b1;
+    // RT_TEX_RC: both quotients on the host's correctly rounded 1/areaABC
+    // (div_core0: the exact IEEE quotient for areaABC in [2^-400, 2^400] and a
+    // numerator 0 or of magnitude in [2^-500, 2^500]); other lanes divide
+    const double aPBC = fabs(areaPBC), aPCA = fabs(areaPCA), aABC = fabs(areaABC);
+    if (RT_TRI_UNORM && RT_TEX_RC && aABC >= 0x1p-400 && aABC <= 0x1p400 &&
+        (aPBC == 0.0 || (aPBC >= 0x1p-500 && aPBC <= 0x1p500)) && (aPCA == 0.0 || (aPCA >= 0x1p-500 && aPCA <= 0x1p500))) {
+        b0 = div_core0(areaPBC, areaABC, tx.rarea);
+        b1 = div_core0(areaPCA, areaABC, tx.rarea);
+    } else {
+        b0 = areaPBC / areaABC;
+        b1 = areaPCA / areaABC;
+    }
     const double b2 = 1.0 - b0 - b1;
     double u = (b0 * tx.uau + b1 * tx.ubu + b2 * tx.ucu);
     double v = (b0 * tx.uav + b1 * tx.ubv + b2 * tx.ucv);
@@ -1160,8 +1196,7 @@ __device__ __forceinline__ bool cuda_hit(const KParams& kp, const V3 o, const V3
         hn = normalize(hp - v3(s.cx, s.cy, s.cz));   // sphere.hu:31,40
         mat = load_mat(kp.sph_mat + idx);
     } else {
-        const TriGeo g = kp.tri[idx];
-        hn = normalize(v3(g.nx, g.ny, g.nz));            // triangle.hu:266
+        hn = tri_normal(kp, idx);                        // triangle.hu:266
         mat = load_mat(kp.tri_mat + idx);
     }
     return true;
@@ -1380,9 +1415,8 @@ struct LanePath {
                 if (SKY && win == kp.ns - 1) sky_material(kp, win, sg, hp, mat);
             } else {
                 if (COUNT) cnt.c[RT_CNT_TEX_HITS] += 1;
-                const TriGeo tg = kp.tri[win];
                 hp = o + muls(d, best);
-                hn = normalize(v3(tg.nx, tg.ny, tg.nz));
+                hn = tri_normal(kp, win);
                 mat = tri_material(kp, win, hp, hn);
             }
             bool lit = false;
@@ -2114,8 +2148,7 @@ struct QPath {
                         const SphGeo sg = kp.sph[pw];
                         H.hn = normalize(o - v3(sg.cx, sg.cy, sg.cz));
                     } else {
-                        const TriGeo tg = kp.tri[pw];
-                        H.hn = normalize(v3(tg.nx, tg.ny, tg.nz));
+                        H.hn = tri_normal(kp, pw);
                     }
                     H.rs = prs;
                     H.refr = H.hole = false;
@@ -2137,8 +2170,7 @@ struct QPath {
                 const SphGeo sg = kp.sph[win];
                 H.hn = normalize(hp - v3(sg.cx, sg.cy, sg.cz));
             } else {
-                const TriGeo tg = kp.tri[win];
-                H.hn = normalize(v3(tg.nx, tg.ny, tg.nz));
+                H.hn = tri_normal(kp, win);
             }
             const Mat mat = hit_material(kp, hp, H);
             bool lit = false;
