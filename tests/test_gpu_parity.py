@@ -341,6 +341,43 @@ def test_mineways_alpha_holes():
     check_parity(bundle, helpers.params(40, 30, 4, 6))
 
 
+def _zero_uv(tris):
+    for t in tris:
+        for uv in (t.uvA, t.uvB, t.uvC):
+            uv.u = uv.v = 0.0
+
+
+@pytest.mark.parametrize("neg,chunks", [(False, 1), (False, 4), (True, 4)])
+def test_uvless_pyramid_constant_texel(neg, chunks):
+    """Every uv 0 (the texel of each hit is (0, 0) of its material:
+    TriTex::tex0, the kernel's constant-texel path) on the brute-force
+    kernel with the 16x16 refraction texture; -0.0 uvs as well."""
+    bundle = helpers.pyramid_scene()
+    tris = bundle.mesh[0]
+    _zero_uv(tris)
+    if neg:
+        for t in tris:
+            t.uvB.u = -0.0
+            t.uvC.v = -0.0
+    bundle = helpers.SceneBundle(tipe_rt.scenes.cornell_spheres(), bundle.mesh)
+    check_parity(bundle, helpers.params(48, 36, 8, 6, chunks=chunks))
+
+
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_uvless_mineways_bvh_constant_texel(chunks):
+    """The constant-texel path on the BVH queue kernel with 11 16x16
+    textures, alpha holes and refraction (mineways, every uv 0)."""
+    tris, qm, mats, tw, th, nm = tipe_rt.scenes.load_mesh_fixture("mineways")
+    _zero_uv(tris)
+    for t in tris:
+        for P in (t.A, t.B, t.C):
+            P.e[0] = P.e[0] * 0.1 - 0.2
+            P.e[1] = P.e[1] * 0.1 - 1.0
+            P.e[2] = P.e[2] * 0.1 - 2.5
+    bundle = helpers.SceneBundle(tipe_rt.scenes.cornell_spheres(), (tris, qm, mats, tw, th, nm))
+    check_parity(bundle, helpers.params(40, 30, 4, 6, use_ao=True, chunks=chunks))
+
+
 def test_tree_ao_c4_scene():
     """C4 scene: README spheres + 1tree_tri.obj (1320 tris,
     Kd-flat materials, leaves = material 1 -> emitter override), AO on with
