@@ -786,7 +786,6 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         // get_barycentric_coord's areaABC (texture.h:18) with the hit normal n = un:
         // dot(n, cross(B - A, C - A)) = dot(un, N), constant per triangle
         x.area = (x.unx * g.nx + x.uny * g.ny) + x.unz * g.nz;
-        x.rarea = 1.0 / x.area;
         tri_mat[i] = to_dev(t.mat);
     }
     // Triangle BVH (rt_bvh.cpp) over scenes with more than 32 triangles; the

@@ -10,7 +10,7 @@
 //                          (winner, fallback scan; r2 = -inf padding)
 //   DevMat  [ns]     80 B  sphere material — gathered for the winner only
 //   TriGeo  [nt]     96 B  A, B-A, C-A, N  — scanned wave-uniformly
-//   TriTex  [nt]    144 B  B, C, uvA/B/C, material, unit normal, area terms — winner only
+//   TriTex  [nt]    136 B  B, C, uvA/B/C, material, unit normal, area terms — winner only
 //   BvhNode4[nodes] 128 B  four child boxes (rt_bvh.h) when nt > 32; the
 //   int     [nt]           triangle arrays are then in leaf order and
 //                          tri_orig maps back to the caller's order
@@ -53,13 +53,12 @@ struct TriTex {                                       // what tri_uvmapping read
                              // material mat for any finite hit), else -1
     double unx, uny, unz;    // vec3_normalize(N) (mesh.h:91), host-computed: the hit normal
     double area;             // get_barycentric_coord's areaABC = dot(un, N) (texture.h:18)
-    double rarea;            // 1 / area, correctly rounded (div_core's reciprocal)
 };
 static_assert(sizeof(SphGeo) == 32, "SphGeo");
 static_assert(sizeof(SphCand) == 32, "SphCand");
 static_assert(sizeof(DevMat) == 80, "DevMat");
 static_assert(sizeof(TriGeo) == 96, "TriGeo");
-static_assert(sizeof(TriTex) == 144, "TriTex");
+static_assert(sizeof(TriTex) == 136, "TriTex");
 
 // uniform block (doubles)
 enum : int {

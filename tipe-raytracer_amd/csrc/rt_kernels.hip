@@ -120,9 +120,6 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_TEX_CONST                // uv-less triangles take their constant texel (TriTex::tex0; A/B knob)
 #define RT_TEX_CONST 1
 #endif
-#ifndef RT_TEX_RC                   // texel barycentrics divide on the host's 1/areaABC (A/B knob)
-#define RT_TEX_RC 0
-#endif
 #ifndef RT_WALK_PRIO                // BVH queue kernel: wave priority during its walk steps (0: off).  The walk
 #define RT_WALK_PRIO 2              // is a chain of dependent node/record loads; ahead of the other waves'
 #endif                              // VALU it issues sooner: C4 +2.0..2.4 %, sweep +1.7..2.6 % (levels 1-3
@@ -997,19 +994,8 @@ __device__ __forceinline__ TexRef tri_texel(const KParams& kp, int k, const V3 P
     const double areaABC = RT_TRI_UNORM ? tx.area : dot(n, v3(g.nx, g.ny, g.nz));
     const double areaPBC = dot(n, cross(B - P, C - P));
     const double areaPCA = dot(n, cross(C - P, A - P));
-    double b0, b1;
-    // RT_TEX_RC: both quotients on the host's correctly rounded 1/areaABC
-    // (div_core0: the exact IEEE quotient for areaABC in [2^-400, 2^400] and a
-    // numerator 0 or of magnitude in [2^-500, 2^500]); other lanes divide
-    const double aPBC = fabs(areaPBC), aPCA = fabs(areaPCA), aABC = fabs(areaABC);
-    if (RT_TRI_UNORM && RT_TEX_RC && aABC >= 0x1p-400 && aABC <= 0x1p400 &&
-        (aPBC == 0.0 || (aPBC >= 0x1p-500 && aPBC <= 0x1p500)) && (aPCA == 0.0 || (aPCA >= 0x1p-500 && aPCA <= 0x1p500))) {
-        b0 = div_core0(areaPBC, areaABC, tx.rarea);
-        b1 = div_core0(areaPCA, areaABC, tx.rarea);
-    } else {
-        b0 = areaPBC / areaABC;
-        b1 = areaPCA / areaABC;
-    }
+    const double b0 = areaPBC / areaABC;
+    const double b1 = areaPCA / areaABC;
     const double b2 = 1.0 - b0 - b1;
     double u = (b0 * tx.uau + b1 * tx.ubu + b2 * tx.ucu);
     double v = (b0 * tx.uav + b1 * tx.ubv + b2 * tx.ucv);
