@@ -117,6 +117,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_TRI_UNORM                // triangle hits read the host-normalized normal (A/B knob)
 #define RT_TRI_UNORM 1
 #endif
+#ifndef RT_MERGED_NRM               // AO queue kernels: one normal computation per round for hit lanes and
+#define RT_MERGED_NRM 1             // pending bounces (A/B knob; C4 +2.4 %)
+#endif
 #ifndef RT_TEX_CONST                // uv-less triangles take their constant texel (TriTex::tex0; A/B knob)
 #define RT_TEX_CONST 1
 #endif
@@ -2104,60 +2107,28 @@ struct QPath {
 
     // After a cast (state SM_RESOLVE).  Returns the role for next_ray, or
     // ROLE_NONE; a lane whose path is over gets state SM_CAM (sum added).
+    // the normal of a hit at point p: sphere (hit_sphere's normalize(p - C),
+    // sphere.h:33) or triangle (tri_normal)
+    __device__ __forceinline__ static V3 hit_normal(const KParams& kp, V3 p, int k, int w)
+    {
+        if (NT || k == HIT_SPHERE) {
+            const SphGeo sg = kp.sph[w];
+            return normalize(p - v3(sg.cx, sg.cy, sg.cz));
+        }
+        return tri_normal(kp, w);
+    }
+
     __device__ __forceinline__ int resolve_hit(const KParams& kp, double* acc, QHit& H, uint32_t sn)
     {
-        bool ended = false, add_inc = true;
+        // (AO kernels only: without AO there is no second normal; C2 -0.7 % there)
+        constexpr bool MN = RT_MERGED_NRM && AOM == AO_ON;
+        bool ended = false, add_inc = true, hit = false, nrm = false;
+        V3 np = v3(0, 0, 0);
+        int nk = HIT_NONE, nw = 0;
         int role = ROLE_NONE;
-        if (AOM == AO_ON && ao_cast) {
-            // ambient_occlusion's tail, main.c:104-115
-            const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
-            double occ = 0.0;
-            if (kind != HIT_NONE) {
-                const V3 hp = o + muls(cast_dir(), best);
-                const V3 df = hp - o;
-                const double distance = sqrt(dot(df, df));
-                double att = distance / best;
-                att = pm_pow(att, AO);
-                occ = occ + att;
-            }
-            occ = (occ / 1.0) / AO;
-            const V3 r2 = mulv(rc_get(), v3(occ, occ, occ));
-            rc_set(r2);
-            ao_cast = false;
-            ++i;                                         // the bounce after the AO cast
-            ended = zero_rc_of(kp, r2) || i >= kp.B;
-            if (!ended) {
-                if (pend) {                              // its direction is still to be made
-                    role = ROLE_PBOUNCE;
-                    const int pw = pkw & 0x3fffffff;     // the bounce hit's normal (o is its hit point)
-                    if (NT || (pkw >> 30) == HIT_SPHERE) {
-                        const SphGeo sg = kp.sph[pw];
-                        H.hn = normalize(o - v3(sg.cx, sg.cy, sg.cz));
-                    } else {
-                        H.hn = tri_normal(kp, pw);
-                    }
-                    H.rs = prs;
-                    H.refr = H.hole = false;
-                } else {
-                    cd = d;
-                    state = SM_CAST;
-                }
-            }
-            pend = false;
-        } else if (kind == HIT_NONE) {                   // miss: the path ends, main.c:236-238
-            if (chain) {
-                acc_add(acc, ACC_ALB, v3(0, 0, 0));
-                acc_add(acc, ACC_NRM, v3(0, 0, 0));
-            }
-            ended = true;
-        } else {
-            const V3 hp = o + muls(d, best);             // ray_at
-            if (NT || kind == HIT_SPHERE) {
-                const SphGeo sg = kp.sph[win];
-                H.hn = normalize(hp - v3(sg.cx, sg.cy, sg.cz));
-            } else {
-                H.hn = tri_normal(kp, win);
-            }
+        // a hit's material, chain sums, emitter / hole / refraction / shading and
+        // the next role (main.c:137-234), H.hn set
+        auto hit_rest = [&](const V3 hp) __attribute__((always_inline)) {
             const Mat mat = hit_material(kp, hp, H);
             bool lit = false;
             if (chain) {
@@ -2210,7 +2181,72 @@ struct QPath {
                     }
                 }
             }
+        };
+        if (AOM == AO_ON && ao_cast) {
+            // ambient_occlusion's tail, main.c:104-115
+            const double AO = ((cdptr)kp.uni)[opq0() + U_AO];
+            double occ = 0.0;
+            if (kind != HIT_NONE) {
+                const V3 hp = o + muls(cast_dir(), best);
+                const V3 df = hp - o;
+                const double distance = sqrt(dot(df, df));
+                double att = distance / best;
+                att = pm_pow(att, AO);
+                occ = occ + att;
+            }
+            occ = (occ / 1.0) / AO;
+            const V3 r2 = mulv(rc_get(), v3(occ, occ, occ));
+            rc_set(r2);
+            ao_cast = false;
+            ++i;                                         // the bounce after the AO cast
+            ended = zero_rc_of(kp, r2) || i >= kp.B;
+            if (!ended) {
+                if (pend) {                              // its direction is still to be made
+                    role = ROLE_PBOUNCE;
+                    const int pw = pkw & 0x3fffffff;     // the bounce hit's normal (o is its hit point)
+                    if (MN) {                            // below, with the hit lanes' normals
+                        np = o;
+                        nw = pw;
+                        nk = pkw >> 30;
+                        nrm = true;
+                    } else if (NT || (pkw >> 30) == HIT_SPHERE) {
+                        const SphGeo sg = kp.sph[pw];
+                        H.hn = normalize(o - v3(sg.cx, sg.cy, sg.cz));
+                    } else {
+                        H.hn = tri_normal(kp, pw);
+                    }
+                    H.rs = prs;
+                    H.refr = H.hole = false;
+                } else {
+                    cd = d;
+                    state = SM_CAST;
+                }
+            }
+            pend = false;
+        } else if (kind == HIT_NONE) {                   // miss: the path ends, main.c:236-238
+            if (chain) {
+                acc_add(acc, ACC_ALB, v3(0, 0, 0));
+                acc_add(acc, ACC_NRM, v3(0, 0, 0));
+            }
+            ended = true;
+        } else {
+            if (MN) {                                    // the rest after the merged normal below
+                hit = true;
+                np = o + muls(d, best);                  // ray_at
+                nw = win;
+                nk = kind;
+                nrm = true;
+            } else {
+                const V3 hp = o + muls(d, best);         // ray_at
+                H.hn = hit_normal(kp, hp, kind, win);
+                hit_rest(hp);
+            }
         }
+        // RT_MERGED_NRM: the normal of the hit each lane goes on from -- this cast's,
+        // or the bounce hit waiting for the AO cast -- in ONE normalize for the
+        // wave instead of one per branch
+        if (MN && nrm) H.hn = hit_normal(kp, np, nk, nw);
+        if (MN && hit) hit_rest(np);
         if (ended) {
             if (add_inc) acc_add(acc, ACC_RAD, inc_get());
             ++s;
