@@ -161,6 +161,14 @@ struct Stream {
         ++n;
         return w >> 1;
     }
+    // next31 for a draw whose block the caller already put in the cache (slot 0
+    // included)
+    __device__ __forceinline__ uint32_t next31_cached()
+    {
+        const uint32_t w = cache[(n & 3u) * 256];
+        ++n;
+        return w >> 1;
+    }
 };
 
 // rand()/(RAND_MAX + 1.0), rtutility.h:192

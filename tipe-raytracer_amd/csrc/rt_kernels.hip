@@ -120,6 +120,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_MERGED_NRM               // AO queue kernels: one normal computation per round for hit lanes and
 #define RT_MERGED_NRM 1             // pending bounces (A/B knob; C4 +2.4 %)
 #endif
+#ifndef RT_REFR_PREFETCH            // queue kernels: the refraction draw's Philox block made in the round's
+#define RT_REFR_PREFETCH 1          // shared Philox step (A/B knob)
+#endif
 #ifndef RT_TEX_CONST                // uv-less triangles take their constant texel (TriTex::tex0; A/B knob)
 #define RT_TEX_CONST 1
 #endif
@@ -2301,7 +2304,8 @@ struct QPath {
                 top_n2 = mat.ior;
             }
             const V3 rf = refracted(d, nn, n1, n2);
-            const double rnd = 0.0 + 1.0 * unit31(st.next31());
+            // (RT_REFR_PREFETCH) the draw is in the block cache whatever its slot
+            const double rnd = 0.0 + 1.0 * unit31(RT_REFR_PREFETCH ? st.next31_cached() : st.next31());
             if (rnd > mat.alpha) {
                 d = rf;
                 shaded = false;
@@ -2609,13 +2613,19 @@ void render_kernel_q(const KParams kp)
             } else {
                 if (!cam && !aor && sa != 0u) wa = rng[sa * 256];          // cached word of the current block
                 if (!cam && !aor && sb != 0u && sa != 0u) wb = rng[sb * 256];
-                if (cam || aor || sa == 0u || sb == 0u) {                 // a new block: one Philox for every role
-                    const uint32_t bi = cam ? 0u : ((nd + (sa == 0u ? 0u : 1u)) >> 2);
+                // RT_REFR_PREFETCH: a refraction lane whose direction draws are
+                // both cached (n = 2 mod 4) but whose refraction draw n+2 opens
+                // the next block makes that block here, in the round's one Philox,
+                // instead of in finish_bounce's own (a second Philox per round)
+                const bool rpre = RT_REFR_PREFETCH && !cam && !aor && !pbr && H.refr && sa == 2u;
+                if (cam || aor || sa == 0u || sb == 0u || rpre) {         // a new block: one Philox for every role
+                    const uint32_t bi = cam ? 0u : ((nd + (sa == 0u ? 0u : rpre ? 2u : 1u)) >> 2);
                     blk = philox4x32_10(bi, 0u, pixel, (uint32_t)(kp.s_base + L.s), kp.key0, kp.key1);
                     if (aor) {                                      // the bounce's draws, for ROLE_PBOUNCE
                         rng[0] = blk.w0;
                         rng[256] = blk.w1;
                     } else if (!cam) {                              // keep the rest of the block
+                        if (rpre) rng[0] = blk.w0;
                         rng[256] = blk.w1;
                         rng[512] = blk.w2;
                         rng[768] = blk.w3;
