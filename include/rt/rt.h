@@ -438,6 +438,18 @@ int rt_verify_sphere_pass(const rt_scene* scene, const double* rays, long long n
  * correctness bar).  Synchronous, device 0. */
 int rt_verify_normalize(unsigned long long seed, unsigned long long n, unsigned long long counts[2]);
 
+/* Stress check of the texel lookup's affine fast path (tri_uvmapping +
+ * get_barycentric_coord, texture.h:16-27,44-90): point i (3 doubles in pts)
+ * taken as a hit on triangle tri[i] of the scene (at most 32 triangles, so in
+ * the caller's order; the hit normal is the triangle's unit normal) through the
+ * affine uv map when its rounding bound makes the texel certain, against the
+ * reference's barycentric operations.  counts[0] = points the fast path
+ * decides, counts[1] = points where it picks another texel (0 is the
+ * correctness bar).  A scene whose triangles all have uv 0 has no map
+ * (RT_EUNSUPPORTED).  Synchronous, device 0. */
+int rt_verify_texel_map(const rt_scene* scene, const double* pts, const int* tri, long long n,
+                        unsigned long long counts[2]);
+
 #ifdef __cplusplus
 }
 #endif

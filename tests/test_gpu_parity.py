@@ -378,6 +378,39 @@ def test_uvless_mineways_bvh_constant_texel(chunks):
     check_parity(bundle, helpers.params(40, 30, 4, 6, use_ao=True, chunks=chunks))
 
 
+def _textured_quad(tw, th, u0, v0, su, sv, seed):
+    """Two triangles filling the view at z = -2 (front-facing), uv from
+    (u0, v0) over (su, sv) (several repeats, negative too), and a tw x th
+    table of random opaque texels."""
+    from tipe_rt.scenes import material
+    rng = np.random.default_rng(seed)
+    P = [(-1.5, -1.5, -2.0), (1.5, -1.5, -2.0), (1.5, 1.5, -2.0), (-1.5, 1.5, -2.0)]
+    UVs = [(u0, v0), (u0 + su, v0), (u0 + su, v0 + sv), (u0, v0 + sv)]
+    tris = (Triangle * 2)()
+    for t, (a, b, c) in zip(tris, [(0, 1, 2), (0, 2, 3)]):
+        for name, i in (("A", a), ("B", b), ("C", c)):
+            getattr(t, name).e[:] = P[i]
+            uv = getattr(t, "uv" + name)
+            uv.u, uv.v = UVs[i]
+        t.mat = material((0.5, 0.5, 0.5))
+    qm = (C.c_int * 2)(0, 0)
+    mats = (Material * (tw * th))()
+    for k in range(tw * th):
+        mats[k] = material(tuple(rng.uniform(0.05, 0.95, 3)))
+    return tris, qm, mats, tw, th, 1
+
+
+@pytest.mark.parametrize("tw,th,u0,v0,su,sv,chunks", [(16, 16, -1.3, -0.6, 3.7, 2.9, 1), (16, 16, 0.25, 0.5, 7.0, 5.0, 4),
+                                                      (5, 3, -2.1, 0.3, 4.4, 3.3, 4)])
+def test_textured_quad_texel_boundaries(tw, th, u0, v0, su, sv, chunks):
+    """Thousands of texture hits at and near texel boundaries and integer uv
+    wraps (uv spans several repeats, negatives included, 0.25-aligned
+    corners): tri_texel's affine fast path and its exact fallback against the
+    oracle's exact barycentric path, bit for bit."""
+    bundle = helpers.SceneBundle(tipe_rt.scenes.cornell_spheres(), _textured_quad(tw, th, u0, v0, su, sv, 7))
+    check_parity(bundle, helpers.params(96, 72, 4, 6, chunks=chunks))
+
+
 def test_tree_ao_c4_scene():
     """C4 scene: README spheres + 1tree_tri.obj (1320 tris,
     Kd-flat materials, leaves = material 1 -> emitter override), AO on with
@@ -750,3 +783,62 @@ def test_invalid_arguments_fail_loudly():
     p = helpers.params(8, 6, 1, 5, rng=tipe_rt.RT_RNG_GLIBC)
     rc = tipe_rt.lib().rt_render_rows(C.byref(bundle.scene), C.byref(p), 5, 0, canva.ctypes.data, None, None)
     assert rc == tipe_rt.RT_EUNSUPPORTED
+
+
+@pytest.mark.parametrize("tw,th", [(16, 16), (3, 1), (64, 5), (1, 1)])
+def test_texel_map_fast_path_stress(tw, th):
+    """rt_verify_texel_map: the affine uv fast path (rt_api.cpp tri_uv_affine
+    + tri_texel_affine) against the reference's barycentric operations on
+    random triangles (scales 1e-3..1e2, far from the origin, skinny ones),
+    random and grid-aligned uvs (boundaries through structured points, uv
+    repeats, negatives), and points in and around each triangle (barycentric
+    coordinates on a 1/16 grid and random ones, off the plane by up to the
+    triangle's size): no point may get another texel, and the fast path must
+    decide almost every point."""
+    from tipe_rt.scenes import material
+    rng = np.random.default_rng(1000 + tw * 7 + th)
+    total_fast = total = 0
+    for scene_i in range(12):
+        nt = 32
+        tris = (Triangle * nt)()
+        A = np.zeros((nt, 3)); B = np.zeros((nt, 3)); Cc = np.zeros((nt, 3))
+        for k in range(nt):
+            s = 10.0 ** rng.uniform(-3, 2)
+            c = rng.uniform(-1, 1, 3) * (s * 10.0 ** rng.uniform(0, 3))
+            a, b, cc = c + rng.normal(size=3) * s, c + rng.normal(size=3) * s, c + rng.normal(size=3) * s
+            if k % 8 == 7:                                   # skinny: C near the segment AB
+                cc = a + (b - a) * rng.uniform(0.2, 0.8) + rng.normal(size=3) * s * 1e-3
+            A[k], B[k], Cc[k] = a, b, cc
+            for name, v in (("A", a), ("B", b), ("C", cc)):
+                getattr(tris[k], name).e[:] = tuple(v)
+            if k % 2:                                        # grid-aligned uvs: multiples of 1/tw, 1/th
+                uvs = [(rng.integers(-2 * tw, 3 * tw) / tw, rng.integers(-2 * th, 3 * th) / th) for _ in range(3)]
+            else:
+                uvs = [tuple(rng.uniform(-3, 6, 2)) for _ in range(3)]
+            for name, (u, v) in zip(("uvA", "uvB", "uvC"), uvs):
+                getattr(tris[k], name).u, getattr(tris[k], name).v = u, v
+            tris[k].mat = material((0.5, 0.5, 0.5))
+        qm = (C.c_int * nt)(*([0] * nt))
+        mats = (Material * (tw * th))()
+        for i in range(tw * th):
+            mats[i] = material((0.5, 0.5, 0.5))
+        scene = tipe_rt.make_scene(tipe_rt.scenes.cornell_spheres(), tris, qm, mats, tw, th, 1)
+        m = 1 << 16
+        tri = rng.integers(0, nt, m)
+        grid = rng.integers(-3, 20, (m, 2)) / 16.0
+        rnd = rng.uniform(-0.2, 1.2, (m, 2))
+        bc = np.where((np.arange(m) % 2 == 0)[:, None], grid, rnd)
+        b0, b1 = bc[:, 0], bc[:, 1]
+        b2 = 1.0 - b0 - b1
+        P = b0[:, None] * A[tri] + b1[:, None] * B[tri] + b2[:, None] * Cc[tri]
+        N = np.cross(B[tri] - A[tri], Cc[tri] - A[tri])
+        nl = np.linalg.norm(N, axis=1)[:, None]
+        size = np.max(np.abs(np.stack([B[tri] - A[tri], Cc[tri] - A[tri]])), axis=(0, 2))[:, None]
+        off = np.where((np.arange(m) % 3 == 0)[:, None], 0.0, rng.uniform(-1, 1, (m, 1)) * size)
+        P = P + off * N / np.where(nl > 0, nl, 1.0)
+        fast, bad = tipe_rt.verify_texel_map(scene, P, tri)
+        assert bad == 0, (scene_i, fast, bad)
+        total_fast += fast
+        total += m
+    print("texel map fast path: %d of %d points" % (total_fast, total))
+    assert total_fast >= 0.5 * total, (total_fast, total)

@@ -140,6 +140,7 @@ struct rt_device_scene {
     DevMat* sph_mat = nullptr;
     TriGeo* tri = nullptr;
     TriTex* tri_tex = nullptr;
+    TriUV* tri_uv = nullptr;         // affine texel map per triangle (scenes that are not all uv-less)
     DevMat* texels = nullptr;
     BvhNode4* bvh = nullptr;         // 4-wide BVH; null: no BVH (few triangles)
     BvhNodeH* bvhh = nullptr;        // the same tree in 64-byte nodes, or null (does not fit binary16)
@@ -216,6 +217,58 @@ void hsl_roundtrip_host(const rt_vec3& rgb, double out[3])
     out[2] = hue_to_rgb_host(t1, t2, h - third);
 }
 
+// tri_uvmapping's texture coordinates (texture.h:16-27, 44-90) as affine
+// functions of the hit point.  The reference forms b0 = n.((B-P)x(C-P)) / areaABC
+// and b1 = n.((C-P)x(A-P)) / areaABC with n the hit normal (the triangle's unit
+// normal un) and areaABC = TriTex::area; in exact arithmetic b0 = (n.N +
+// ((B-C)x n).(P-A)) / area and b1 = ((C-A)x n).(P-A) / area for EVERY P (the
+// component of P along n cancels in n.((B-P)x(C-P))), so u = uC + b0 (uA-uC) +
+// b1 (uB-uC) = u0 + gu.(P-A).  Rounding bound of the reference's u against that,
+// for P with |P - A|_max <= diam (so every |P - V|_max <= R = 2 diam), Q =
+// |n|_1 R^2 / area, |b_i| <= 2Q: the cross products' components are within 8u R^2,
+// each area within 14u |n|_1 R^2, each b within u (38Q + 3), and u_ref within
+// sum|uv| u (54Q + 7) (u = 2^-53); the kernel's evaluation (three subtractions,
+// three fma, the rounded gradient and u0, the multiplication by tw) adds at most
+// 10u (|u0| + |gu|_1 diam) tw.  Stored: eu = tw (4 x the first + the second)
+// + 4u tw (the reference's own frac * tw rounding) -- in tw units.
+void tri_uv_affine(const TriGeo& g, const TriTex& x, int tw, int th, TriUV& o)
+{
+    typedef long double L;
+    const L u = 0x1p-53L;
+    const L Ax = g.ax, Ay = g.ay, Az = g.az, Bx = x.bx, By = x.by, Bz = x.bz, Cx = x.cx, Cy = x.cy, Cz = x.cz;
+    const L nx = x.unx, ny = x.uny, nz = x.unz, area = x.area;
+    const L nN = nx * (L)g.nx + ny * (L)g.ny + nz * (L)g.nz;
+    const L dmax = std::max({std::fabs(Bx - Ax), std::fabs(By - Ay), std::fabs(Bz - Az), std::fabs(Cx - Ax),
+                             std::fabs(Cy - Ay), std::fabs(Cz - Az), std::fabs(Cx - Bx), std::fabs(Cy - By),
+                             std::fabs(Cz - Bz)});
+    o = TriUV{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1.0};
+    if (!(area > 0) || !std::isfinite((double)area) || !(dmax > 0) || !std::isfinite((double)dmax)) return;
+    // grad b0 = (B - C) x n / area, grad b1 = (C - A) x n / area
+    const L p0x = (By - Cy) * nz - (Bz - Cz) * ny, p0y = (Bz - Cz) * nx - (Bx - Cx) * nz, p0z = (Bx - Cx) * ny - (By - Cy) * nx;
+    const L p1x = (Cy - Ay) * nz - (Cz - Az) * ny, p1y = (Cz - Az) * nx - (Cx - Ax) * nz, p1z = (Cx - Ax) * ny - (Cy - Ay) * nx;
+    const L b0A = nN / area;                 // b0 at A (1 up to areaABC's rounding), b1 at A = 0
+    const L uA = x.uau, uB = x.ubu, uC = x.ucu, vA = x.uav, vB = x.ubv, vC = x.ucv;
+    const L gux = (p0x * (uA - uC) + p1x * (uB - uC)) / area, guy = (p0y * (uA - uC) + p1y * (uB - uC)) / area,
+            guz = (p0z * (uA - uC) + p1z * (uB - uC)) / area;
+    const L gvx = (p0x * (vA - vC) + p1x * (vB - vC)) / area, gvy = (p0y * (vA - vC) + p1y * (vB - vC)) / area,
+            gvz = (p0z * (vA - vC) + p1z * (vB - vC)) / area;
+    const L u0 = uC + b0A * (uA - uC), v0 = vC + b0A * (vA - vC);
+    const L R = 2 * dmax;
+    const L n1 = std::fabs(nx) + std::fabs(ny) + std::fabs(nz);
+    const L Q = n1 * R * R / area;
+    const L su = std::fabs(uA) + std::fabs(uB) + std::fabs(uC), sv = std::fabs(vA) + std::fabs(vB) + std::fabs(vC);
+    const L gu1 = std::fabs(gux) + std::fabs(guy) + std::fabs(guz), gv1 = std::fabs(gvx) + std::fabs(gvy) + std::fabs(gvz);
+    const L mu = std::fabs(u0) + gu1 * dmax, mv = std::fabs(v0) + gv1 * dmax;   // |u(P)|, |v(P)| bounds
+    const L eu = tw * (4 * su * u * (54 * Q + 7) + 10 * u * mu + 4 * u);
+    const L ev = th * (4 * sv * u * (54 * Q + 7) + 10 * u * mv + 4 * u);
+    // the kernel converts floor(tw u) to int: keep |tw u| well inside 2^31
+    if (!std::isfinite((double)eu) || !std::isfinite((double)ev) || tw * mu > 0x1p29L || th * mv > 0x1p29L ||
+        eu > 0.25L || ev > 0.25L)
+        return;
+    o = TriUV{(double)gux, (double)guy, (double)guz, (double)u0, (double)gvx, (double)gvy, (double)gvz, (double)v0,
+              (double)(eu * (1 + 0x1p-20L)), (double)(ev * (1 + 0x1p-20L)), (double)dmax};
+}
+
 DevMat to_dev(const rt_material& m)
 {
     return DevMat{m.diffuseColor.e[0],  m.diffuseColor.e[1],  m.diffuseColor.e[2], m.emissionColor.e[0],
@@ -232,6 +285,7 @@ void free_scene(rt_device_scene* s)
     (void)hipFree(s->sph_mat);
     (void)hipFree(s->tri);
     (void)hipFree(s->tri_tex);
+    (void)hipFree(s->tri_uv);
     (void)hipFree(s->texels);
     (void)hipFree(s->bvh);
     (void)hipFree(s->bvhh);
@@ -272,6 +326,7 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     kp.sph_mat = sc->sph_mat;
     kp.tri = sc->tri;
     kp.tri_tex = sc->tri_tex;
+    kp.tri_uv = sc->tri_uv;
     kp.texels = sc->texels;
     kp.tri_orig = sc->tri_orig;
     kp.sph_rinv = sc->sph_rinv;
@@ -858,6 +913,13 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->coord_max = coord_max;
     ds->all_tex0 = scene->nbTriangles > 0 &&
                    std::all_of(tex.begin(), tex.end(), [](const TriTex& x) { return x.tex0 >= 0; });
+    // the affine texel map (rt_kernels.hip tri_texel's fast path), in leaf order
+    std::vector<TriUV> tri_uv;
+    if (scene->nbTriangles > 0 && !ds->all_tex0) {
+        tri_uv.resize(tex.size());
+        for (size_t i = 0; i < tex.size(); ++i)
+            tri_uv_affine(tri[i], tex[i], scene->tex_width, scene->tex_height, tri_uv[i]);
+    }
     ds->ns = scene->nbSpheres;
     ds->ns_pad = ns_pad;
     ds->cand_lmax = cand_lmax;
@@ -891,7 +953,7 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
             nodesh.clear();
     }
     if ((rc = upload(&ds->sph, sph)) || (rc = upload(&ds->sph_cand, cand)) || (rc = upload(&ds->sph_mat, sph_mat)) || (rc = upload(&ds->tri, tri)) ||
-        (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->texels, texels)) ||
+        (rc = upload(&ds->tri_tex, tex)) || (rc = upload(&ds->tri_uv, tri_uv)) || (rc = upload(&ds->texels, texels)) ||
         (rc = upload(&ds->bvh, bvh.nodes4)) || (rc = upload(&ds->bvhh, nodesh)) || (rc = upload(&ds->tri_orig, bvh.order)) ||
         (rc = upload(&ds->sky, sky)) || (rc = upload(&ds->sph_rinv, sph_rinv)) || (rc = upload(&ds->sph_disp, sph_disp)) ||
         (rc = upload(&ds->tri_mat, tri_mat))) {
@@ -1541,6 +1603,59 @@ int rt_verify_sphere_pass(const rt_scene* scene, const double* rays, long long n
     (void)hipFree(d);
     rt_scene_release(ds);
     if (e != hipSuccess) return fail(RT_EDEVICE, "verify_sphere_pass: %s", hipGetErrorString(e));
+    return RT_OK;
+}
+
+int rt_verify_texel_map(const rt_scene* scene, const double* pts, const int* tri, long long n,
+                        unsigned long long counts[2])
+{
+    if (!counts || !pts || !tri || n < 0 || !scene) return fail(RT_EINVAL, "bad verify arguments");
+    counts[0] = counts[1] = 0;
+    if (scene->nbTriangles < 1 || scene->nbTriangles > 32)
+        return fail(RT_EUNSUPPORTED, "verify_texel_map: 1-32 triangles (caller order), got %d", scene->nbTriangles);
+    for (long long i = 0; i < n; ++i)
+        if (tri[i] < 0 || tri[i] >= scene->nbTriangles) return fail(RT_EINVAL, "tri[%lld] = %d", i, tri[i]);
+    if (n == 0) return RT_OK;
+    int dev = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        int rc = ensure_init_locked();
+        if (rc) return rc;
+        dev = g_devices[0];
+    }
+    rt_device_scene* ds = nullptr;
+    int rc = rt_scene_upload(dev, scene, &ds);
+    if (rc) return rc;
+    if (!ds->tri_uv) {
+        rt_scene_release(ds);
+        return fail(RT_EUNSUPPORTED, "verify_texel_map: the scene has no affine texel map (every uv 0)");
+    }
+    DeviceGuard guard(dev);
+    KParams kp;
+    std::memset(&kp, 0, sizeof kp);
+    kp.tri = ds->tri;
+    kp.tri_tex = ds->tri_tex;
+    kp.tri_uv = ds->tri_uv;
+    kp.tw = ds->tw;
+    kp.th = ds->th;
+    kp.n_texels = ds->n_texels;
+    double* d_pts = nullptr;
+    int* d_tri = nullptr;
+    unsigned long long* d = nullptr;
+    hipError_t e = hipMalloc((void**)&d_pts, (size_t)n * 3 * sizeof(double));
+    if (e == hipSuccess) e = hipMalloc((void**)&d_tri, (size_t)n * sizeof(int));
+    if (e == hipSuccess) e = hipMalloc((void**)&d, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemcpy(d_pts, pts, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_tri, tri, (size_t)n * sizeof(int), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemset(d, 0, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = (hipError_t)launch_verify_texel(kp, d_pts, d_tri, n, d);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(counts, d, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    (void)hipFree(d_pts);
+    (void)hipFree(d_tri);
+    (void)hipFree(d);
+    rt_scene_release(ds);
+    if (e != hipSuccess) return fail(RT_EDEVICE, "verify_texel_map: %s", hipGetErrorString(e));
     return RT_OK;
 }
 

@@ -59,6 +59,17 @@ static_assert(sizeof(SphCand) == 32, "SphCand");
 static_assert(sizeof(DevMat) == 80, "DevMat");
 static_assert(sizeof(TriGeo) == 96, "TriGeo");
 static_assert(sizeof(TriTex) == 136, "TriTex");
+// tri_uvmapping's u, v as affine functions of the hit point (rt_api.cpp
+// tri_uv_affine): u(P) = u0 + gu.(P - A), v(P) = v0 + gv.(P - A), with
+// tw*|u_ref - u| <= eu (th*|v_ref - v| <= ev) for every P within diam
+// (max-norm) of A, u_ref being the reference's rounded u; diam < 0: no fast
+// path for this triangle
+struct TriUV {
+    double gux, guy, guz, u0;
+    double gvx, gvy, gvz, v0;
+    double eu, ev, diam;
+};
+static_assert(sizeof(TriUV) == 88, "TriUV");
 
 // uniform block (doubles)
 enum : int {
@@ -77,6 +88,7 @@ struct KParams {
     const DevMat* sph_mat;
     const TriGeo* tri;
     const TriTex* tri_tex;
+    const TriUV* tri_uv;     // (textured scenes) the affine texel map, null: every hit takes the exact path
     const DevMat* texels;
     const double* uni;       // U_COUNT doubles
     const BvhNode4* bvh;     // 4-wide triangle BVH (rt_bvh.h), or null: brute-force scan
@@ -152,6 +164,8 @@ int launch_selftest(int op, const double* d_in, double* d_out, int n, void* stre
 int launch_verify_phi(unsigned long long r0, unsigned long long n, unsigned long long* d_counts);
 int launch_verify_normalize(unsigned long long seed, unsigned long long n, unsigned long long* d_counts);
 int launch_verify_spheres(const KParams& kp, const double* d_rays, long long n, unsigned long long* d_counts);
+int launch_verify_texel(const KParams& kp, const double* d_pts, const int* d_tri, long long n,
+                        unsigned long long* d_counts);
 int launch_resolve(const KParams& kp, void* stream);
 int launch_denoise_pack(long long npx, const double* canva, const double* albedo, const double* normal,
                         float* color3, float* albedo3, float* normal3, void* stream);

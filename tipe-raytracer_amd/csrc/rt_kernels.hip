@@ -123,6 +123,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_REFR_PREFETCH            // queue kernels: the refraction draw's Philox block made in the round's
 #define RT_REFR_PREFETCH 1          // shared Philox step (A/B knob)
 #endif
+#ifndef RT_TEX_AFFINE               // texel lookups through the host's affine uv map when certain (A/B knob)
+#define RT_TEX_AFFINE 1
+#endif
 #ifndef RT_TEX_CONST                // uv-less triangles take their constant texel (TriTex::tex0; A/B knob)
 #define RT_TEX_CONST 1
 #endif
@@ -171,6 +174,15 @@ __device__ __forceinline__ double dmin_abs3(double a, double b, double c)
 {
     double r;
     asm("v_min_f64 %0, |%1|, |%2|\n\tv_min_f64 %0, %0, |%3|" : "=&v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// max(|a|, |b|, |c|) (a NaN operand drops out: callers test the values it
+// bounds for NaN themselves)
+__device__ __forceinline__ double dmax_abs3(double a, double b, double c)
+{
+    double r;
+    asm("v_max_f64 %0, |%1|, |%2|\n\tv_max_f64 %0, %0, |%3|" : "=&v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
 }
 
@@ -988,10 +1000,35 @@ __device__ __forceinline__ V3 tri_normal(const KParams& kp, int k)
     const TriGeo* g = kp.tri + k;
     return normalize(v3(g->nx, g->ny, g->nz));
 }
-__device__ __forceinline__ TexRef tri_texel(const KParams& kp, int k, const V3 P, const V3 n)
+// The texel through the host's affine uv map (rt_api.cpp tri_uv_affine): the
+// reference's u, v are affine in P up to rounding, so with tw*u within eu of tu,
+// x = floor(tw u_ref) - tw floor(u_ref) is certain when no integer lies in
+// [tu - eu, tu + eu] (the wrap at integer u and the cells at multiples of 1/tw
+// are all integers of tw*u); the same for v.  False: not certain (or P farther
+// than diam from A, where the bound does not hold) -- the caller then takes the
+// exact path.  rt_verify_texel_map checks it against tri_texel_exact.
+__device__ __forceinline__ bool tri_texel_affine(const KParams& kp, int k, const V3 P, TexRef& t)
 {
-    if (RT_TEX_CONST && kp.tex_const)            // every uv 0: the texel does not depend on P
-        return TexRef{kp.tri_tex[k].tex0, kp.tri_tex[k].mat};
+    const TriUV q = kp.tri_uv[k];
+    const TriGeo* gp = kp.tri + k;
+    const double dx = P.x - gp->ax, dy = P.y - gp->ay, dz = P.z - gp->az;
+    const double uf = fma(q.gux, dx, fma(q.guy, dy, fma(q.guz, dz, q.u0)));
+    const double vf = fma(q.gvx, dx, fma(q.gvy, dy, fma(q.gvz, dz, q.v0)));
+    const double tw = (double)kp.tw, th = (double)kp.th;
+    const double tu = uf * tw, tv = vf * th;
+    const double lu = floor(tu - q.eu), lv = floor(tv - q.ev);
+    if (!(dmax_abs3(dx, dy, dz) <= q.diam && lu == floor(tu + q.eu) && lv == floor(tv + q.ev))) return false;
+    const int x = (int)fma(-tw, floor(uf), lu), y = (int)fma(-th, floor(vf), lv);
+    const int m = kp.tri_tex[k].mat;
+    long long index = ((long long)y * kp.tw + x) + ((long long)kp.th * kp.tw * m);
+    index = index < 0 ? 0 : index;                       // reference UB -> clamp
+    index = index >= kp.n_texels ? kp.n_texels - 1 : index;
+    t = TexRef{(int)index, m};
+    return true;
+}
+// tri_uvmapping + get_barycentric_coord with the reference's operations
+__device__ __forceinline__ TexRef tri_texel_exact(const KParams& kp, int k, const V3 P, const V3 n)
+{
     const TriGeo g = kp.tri[k];
     const TriTex tx = kp.tri_tex[k];
     const V3 A = v3(g.ax, g.ay, g.az), B = v3(tx.bx, tx.by, tx.bz), C = v3(tx.cx, tx.cy, tx.cz);
@@ -1016,6 +1053,16 @@ __device__ __forceinline__ TexRef tri_texel(const KParams& kp, int k, const V3 P
     index = index < 0 ? 0 : index;                       // reference UB -> clamp
     index = index >= kp.n_texels ? kp.n_texels - 1 : index;
     return TexRef{(int)index, m};
+}
+__device__ __forceinline__ TexRef tri_texel(const KParams& kp, int k, const V3 P, const V3 n)
+{
+    if (RT_TEX_CONST && kp.tex_const)            // every uv 0: the texel does not depend on P
+        return TexRef{kp.tri_tex[k].tex0, kp.tri_tex[k].mat};
+    if (RT_TEX_AFFINE && kp.tri_uv) {
+        TexRef t;
+        if (tri_texel_affine(kp, k, P, t)) return t;
+    }
+    return tri_texel_exact(kp, k, P, n);
 }
 __device__ __forceinline__ Mat texel_material(const KParams& kp, TexRef t)
 {
@@ -3185,6 +3232,39 @@ int launch_verify_normalize(unsigned long long seed, unsigned long long n, unsig
         hipLaunchKernelGGL(verify_normalize_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, nullptr, seed,
                            i0, m, d_counts);
     }
+    return hipGetLastError();
+}
+
+// rt_verify_texel_map: point i (3 doubles) on triangle tri[i] through the
+// affine texel map and through the exact path; counts[0] += certain,
+// counts[1] += certain but a different texel
+__global__ __launch_bounds__(256) void verify_texel_kernel(const KParams kp, const double* __restrict__ pts,
+                                                           const int* __restrict__ tri, long long n,
+                                                           unsigned long long* counts)
+{
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    bool fast = false, bad = false;
+    if (i < n) {
+        const int k = tri[i];
+        const V3 P = v3(pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]);
+        const TexRef e = tri_texel_exact(kp, k, P, tri_normal(kp, k));
+        TexRef f{0, 0};
+        fast = tri_texel_affine(kp, k, P, f);
+        bad = fast && (f.index != e.index || f.m != e.m);
+    }
+    const unsigned long long nf = __popcll(__ballot(fast)), nb = __popcll(__ballot(bad));
+    if ((threadIdx.x & 63) == 0) {
+        if (nf) atomicAdd(counts, nf);
+        if (nb) atomicAdd(counts + 1, nb);
+    }
+}
+
+int launch_verify_texel(const KParams& kp, const double* d_pts, const int* d_tri, long long n,
+                        unsigned long long* d_counts)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(verify_texel_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr, kp, d_pts,
+                       d_tri, n, d_counts);
     return hipGetLastError();
 }
 

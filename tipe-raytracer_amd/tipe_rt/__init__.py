@@ -68,6 +68,8 @@ def lib():
         L.rt_verify_sphere_pass.argtypes = [P(Scene), C.c_void_p, C.c_longlong, C.c_void_p]
         if hasattr(L, "rt_verify_normalize"):    # (older builds in A/B runs lack the diagnostic)
             L.rt_verify_normalize.argtypes = [C.c_ulonglong, C.c_ulonglong, C.c_void_p]
+        if hasattr(L, "rt_verify_texel_map"):
+            L.rt_verify_texel_map.argtypes = [P(Scene), C.c_void_p, C.c_void_p, C.c_longlong, C.c_void_p]
         L.rt_accumulate_async.argtypes = [C.c_void_p, P(Params), C.c_longlong, P(Tiling), C.c_void_p, C.c_void_p]
         L.rt_resolve_async.argtypes = [C.c_void_p, P(Params), C.c_int, P(Tiling), P(Frame), C.c_void_p]
         L.rt_set_denoise_hook.argtypes = [DENOISE_FN]
@@ -91,7 +93,7 @@ EXPORTED_SYMBOLS = ["rt_params_init", "rt_init", "rt_shutdown", "rt_last_error",
                     "rt_scene_release", "rt_render_async", "rt_assemble_async", "rt_count_async",
                     "rt_selftest_math", "rt_accumulate_async", "rt_resolve_async", "rt_set_denoise_hook", "rt_get_denoise_hook", "rt_denoise_pack",
                     "rt_denoise_unpack", "rt_denoise_pack_async", "rt_verify_sampler_phi",
-                    "rt_verify_sphere_pass", "rt_verify_normalize", "rt_set_zero_throughput_exit", "rt_set_fill_spp_chunks", "rt_set_fill_precision",
+                    "rt_verify_sphere_pass", "rt_verify_normalize", "rt_verify_texel_map", "rt_set_zero_throughput_exit", "rt_set_fill_spp_chunks", "rt_set_fill_precision",
                     "rt_scene_cache_clear", "rt_gather_async", "rt_render_gather_async", "rt_peer_access",
                     "rt_last_render_kernel"]
 
@@ -323,6 +325,17 @@ def verify_normalize(seed=1, n=1 << 30):
     a / sqrt(a.a) on n pseudo-random vectors (rt_verify_normalize)."""
     out = (C.c_ulonglong * 2)()
     check(lib().rt_verify_normalize(seed, n, out))
+    return int(out[0]), int(out[1])
+
+
+def verify_texel_map(scene, pts, tri):
+    """(fast-path points, mismatches) of the texel lookup's affine fast path
+    against the reference's barycentric path: pts (n, 3) float64 hit points,
+    tri (n,) their triangles (rt_verify_texel_map)."""
+    p = np.ascontiguousarray(pts, dtype=np.float64)
+    t = np.ascontiguousarray(tri, dtype=np.int32)
+    out = (C.c_ulonglong * 2)()
+    check(lib().rt_verify_texel_map(C.byref(scene), p.ctypes.data, t.ctypes.data, len(p), out))
     return int(out[0]), int(out[1])
 
 
