@@ -1022,6 +1022,10 @@ double oracle_pm_acos(double x) { return pm_acos(x); }
 float oracle_pm_sinf(float x) { return pm_sinf(x); }
 float oracle_pm_cosf(float x) { return pm_cosf(x); }
 double oracle_pm_pow(double x, double y) { return pm_pow(x, y); }
+void oracle_pm_pow_n(const double* xy, double* out, long long n)   /* pairs (x, y) */
+{
+    for (long long i = 0; i < n; ++i) out[i] = pm_pow(xy[2 * i], xy[2 * i + 1]);
+}
 double oracle_pm_atan2(double y, double x) { return pm_atan2(y, x); }
 
 /* texel index sphere_uvmapping picks (test hook; portable: 0 libm, 1 pm_*) */

@@ -81,6 +81,7 @@ def oracle():
         lib.oracle_pm_cosf.restype = C.c_float
         lib.oracle_pm_pow.argtypes = [C.c_double, C.c_double]
         lib.oracle_pm_pow.restype = C.c_double
+        lib.oracle_pm_pow_n.argtypes = [P(C.c_double), P(C.c_double), C.c_longlong]
         lib.oracle_pm_atan2.argtypes = [C.c_double, C.c_double]
         lib.oracle_pm_atan2.restype = C.c_double
         lib.oracle_sky_index.argtypes = [Vec3, C.c_double, Vec3, C.c_int, C.c_int, C.c_int]

@@ -139,6 +139,33 @@ def test_device_pow_special_and_wide_inputs():
     assert same.all(), list(zip(x[~same], y[~same], got[~same], want[~same]))[:6]
 
 
+def _oracle_pow_n(x, y):
+    o = oracle_ffi.oracle()
+    xy = np.ascontiguousarray(np.stack([x, y], 1).ravel())
+    out = np.empty(len(x))
+    o.oracle_pm_pow_n(xy.ctypes.data_as(C.POINTER(C.c_double)), out.ctypes.data_as(C.POINTER(C.c_double)), len(x))
+    return out
+
+
+@pytest.mark.parametrize("y", [2.5, 0.5, 0.1, 1.75, 7.3, 100.5, 999.9, -2.5, 1e-300, 4e6, 1e9])
+def test_device_pow_near1_dense(y):
+    """pm_pow where ambient_occlusion calls it (main.c:109-111: distance / t
+    of the AO hit, 1 up to the rounding of the hit point) against
+    oracle/pm_math.h's pm_pow: every x within 2^15 ulps of 1 on both sides
+    and a random spread out to 2^-26, for AO intensities from 1e-300 to 1e9."""
+    rng = np.random.default_rng(int(abs(y) * 1000) % 2**31)
+    k = np.arange(-2 ** 15, 2 ** 15 + 1, dtype=np.float64)
+    lim = 2.0 ** -26
+    x = np.concatenate([1.0 + k[k >= 0] * 2.0 ** -52, 1.0 + k[k < 0] * 2.0 ** -53,
+                        1.0 + rng.uniform(-lim, lim, 1 << 17), 1.0 + rng.uniform(-(2.0 ** -40), 2.0 ** -40, 1 << 15),
+                        1.0 + np.array([lim, -lim, lim + 2.0 ** -52, -lim - 2.0 ** -53, 2 * lim, 1e-3, -1e-3])])
+    ys = np.full(len(x), y)
+    got = tipe_rt.selftest_math(3, np.stack([x, ys], 1).ravel(), len(x))
+    want = _oracle_pow_n(x, ys)
+    same = got.view(np.uint64) == want.view(np.uint64)
+    assert same.all(), list(zip(x[~same], got[~same], want[~same]))[:6]
+
+
 def test_device_normalize_fast_path_is_ieee():
     """normalize() skips the sqrt/division range fixups on in-range lanes and
     shares 1/|a| (rt_kernels.hip); it must equal a / sqrt(a.a) in IEEE f64

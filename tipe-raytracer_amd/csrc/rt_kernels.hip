@@ -141,7 +141,13 @@ static_assert(!RT_QTASK_TABLE || RT_QUEUE == 64, "the task table holds one batch
 #ifndef RT_WAVES_PER_SIMD_Q         // queue kernel occupancy bound
 #define RT_WAVES_PER_SIMD_Q RT_WAVES_PER_SIMD
 #endif
-#define RT_TRACE_WORDS 4                // RT_QUEUE_TRACE words per lane: start, end, rounds, tasks
+#ifndef RT_PHASE_CLOCK              // diagnostic builds only (tools/phase_clock.py): render_kernel_q adds the
+#define RT_PHASE_CLOCK 0            // wave's s_memtime cycles per round phase to its RT_QUEUE_TRACE record
+#endif
+// RT_QUEUE_TRACE words per lane: start, end, rounds, tasks (+ RT_PHASE_CLOCK:
+// cycles in the sphere cast, the BVH walk, resolve, the task hand-out, and
+// the next-ray step with finish_bounce)
+#define RT_TRACE_WORDS (RT_PHASE_CLOCK ? 9 : 4)
 #ifndef RT_WAVES_PER_SIMD_BVH       // the BVH variant (traversal state + LDS stack)
 #define RT_WAVES_PER_SIMD_BVH 3
 #endif
@@ -2466,8 +2472,21 @@ void render_kernel_q(const KParams kp)
     }
     const long long t_start = kp.trace ? wall_clock64() : 0;
     unsigned rounds = 0, ntasks = 0;
+#if RT_PHASE_CLOCK
+    // wave-uniform clock reads at the round's uniform points (SGPR sums)
+    unsigned long long ph[5] = {0, 0, 0, 0, 0}, tc = __builtin_amdgcn_s_memtime();
+    auto phase = [&](int k) __attribute__((always_inline)) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        ph[k] += t - tc;
+        tc = t;
+    };
+#define RT_PHASE(k) phase(k)
+#else
+#define RT_PHASE(k) ((void)0)
+#endif
     while (true) {
         ++rounds;
+        RT_PHASE(4);                 // the previous round's next-ray step and finish_bounce
         // ---- 1. closest hit (main.c:52-92) for every lane with a ray ------
         if (QB > 0) {
             // spheres, then the triangle BVH: up to QB node visits
@@ -2483,6 +2502,7 @@ void render_kernel_q(const KParams kp)
                 sp = 0;
                 L.state = SM_TRAV;
             }
+            RT_PHASE(0);
             if (__ballot(L.state == SM_TRAV) != 0ull) {
 #if RT_WALK_PRIO
                 __builtin_amdgcn_s_setprio(RT_WALK_PRIO);
@@ -2515,6 +2535,7 @@ void render_kernel_q(const KParams kp)
             L.kind = closest_hit<false, false, false, !SKY && AOM != AO_ON>(kp, L.o, L.cast_dir(), L.best, L.win, cnt);
             L.state = SM_RESOLVE;
         }
+        RT_PHASE(QB > 0 ? 1 : 0);
         // ---- 2. the hit, up to the next direction --------------------------
         int role = ROLE_NONE;
         QHit H;
@@ -2522,6 +2543,7 @@ void render_kernel_q(const KParams kp)
         H.rs = 0.0;
         H.refr = H.hole = false;
         if (L.state == SM_RESOLVE) role = L.resolve_hit(kp, acc, H, st.n);
+        RT_PHASE(2);
         // ---- 3. lanes whose task is done take the next one -----------------
         const bool need = L.state == SM_CAM && L.s >= s1;
         const unsigned long long nm = __ballot(need);
@@ -2633,6 +2655,7 @@ void render_kernel_q(const KParams kp)
             }
         }
         if (__ballot(L.state != SM_DONE) == 0ull) break;     // every lane of the wave is done
+        RT_PHASE(3);
         // tracer with nbRebondMax <= 0 returns (0, 0, 0) albedo/normal/colour
         if (kp.B <= 0 && L.state == SM_CAM && L.s < s1) {
             acc_add(acc, ACC_ALB, v3(0, 0, 0));
@@ -2755,6 +2778,9 @@ void render_kernel_q(const KParams kp)
         q[1] = (unsigned long long)wall_clock64();
         q[2] = rounds;
         q[3] = ntasks;
+#if RT_PHASE_CLOCK
+        for (int k = 0; k < 5; ++k) q[4 + k] = ph[k];
+#endif
     }
 }
 #endif
