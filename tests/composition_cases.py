@@ -31,10 +31,10 @@ PLANES = ("canva", "albedo", "normal", "radiance")
 
 class Case:
     def __init__(self, name, build, W, H, spp, bounces, use_ao=False, ao=0.0, driver="trace_rows",
-                 slow=False, what=""):
+                 slow=False, what="", cam=None):
         self.name, self.build, self.W, self.H = name, build, W, H
         self.spp, self.bounces, self.use_ao, self.ao = spp, bounces, use_ao, ao
-        self.driver, self.slow, self.what = driver, slow, what
+        self.driver, self.slow, self.what, self.cam = driver, slow, what, cam
 
     def scene(self):
         """-> (bundle, params) for the oracle in GLIBC mode."""
@@ -45,11 +45,12 @@ class Case:
             p.spp_chunks = 1
             return bundle, p
         p = helpers.params(self.W, self.H, self.spp, self.bounces, use_ao=self.use_ao, ao=self.ao,
-                           rng=RT_RNG_GLIBC, compat=1 if self.driver == "fill_canva" else 0)
+                           rng=RT_RNG_GLIBC, compat=1 if self.driver == "fill_canva" else 0,
+                           cam=None if self.cam is None else helpers.camera_of(self.cam))
         return b, p
 
 
-def _random(seed):
+def _random(seed, bounce_hi=9):
     """tests/test_gpu_fuzz.random_scene(seed) inside a black, opaque sphere of
     radius 1e4 (appended last).  Without it a primary miss leaves the
     reference's albedo/normal undefined: closest_hit (main.c:54-56) never sets
@@ -60,7 +61,7 @@ def _random(seed):
     def build():
         from test_gpu_fuzz import random_scene     # noqa: WPS433 (shared generator)
         from tipe_rt.types import Sphere, Vec3
-        bundle, p = random_scene(seed)
+        bundle, p = random_scene(seed, bounce_hi=bounce_hi)
         n = len(bundle.spheres)
         sph = (Sphere * (n + 1))()
         for k in range(n):
@@ -109,7 +110,33 @@ CASES = [
          what="C4 scene with AO 2.5 kept as a double"),
 ] + [Case("random_%d" % s, _random(s), 0, 0, 0, 0,
           what="tests/test_gpu_fuzz.random_scene(%d) (aperture, focus, AO, textures, mesh)" % s)
-     for s in range(12)]
+     for s in range(12)] + [
+    # r06: main.c's own default depth nbRebondMax 20 (main.c:310) and 10 (the
+    # nature render, RTX_nature_..._9RB: nbRebondMax - 1 = 9, main.c:328), and
+    # main()'s coordinate regime (camera main.c:300-301, sky sphere 1e5 main.c:346)
+    Case("glass_b20", _glass, 64, 48, 16, 20,
+         what="translucent spheres at main.c's default 20 bounces: deep IOR enter/exit chains"),
+    Case("holes_ao_b20", _holes, 64, 48, 16, 20, use_ao=True, ao=2.0, driver="fill_canva",
+         what="alpha-hole spheres + AO (int 2), 20 bounces"),
+    Case("mineways_b10", helpers.mineways_scene, 64, 48, 16, 10, what="mineways alpha texels, 10 bounces"),
+    Case("mineways_b20", helpers.mineways_scene, 48, 36, 16, 20, what="mineways alpha texels, 20 bounces"),
+    Case("tree_ao_b10", helpers.tree_scene, 48, 36, 8, 10, use_ao=True, ao=2.5, driver="fill_canva",
+         what="C4 tree + AO 2.5 -> int 2 through fill_canva, 10 bounces"),
+    Case("tree_ao_2p5_b20", helpers.tree_scene, 40, 30, 8, 20, use_ao=True, ao=2.5,
+         what="C4 tree + AO 2.5 (double), 20 bounces"),
+    Case("nature_b10", helpers.nature_scene, 48, 36, 8, 10, cam=scenes.NATURE_CAMERA,
+         what="RTX_MAP/nature (5812 tris, 31 textures with alpha, texture.h overrides) + main.c:345-346 "
+              "sun and sky, 10 bounces (the reference render's own depth)"),
+    Case("nature_ao_b20", helpers.nature_scene, 32, 24, 4, 20, use_ao=True, ao=2.5, cam=scenes.NATURE_CAMERA,
+         what="nature + AO 2.5 at main.c's default 20 bounces"),
+    Case("main_regime_b20", helpers.main_regime_scene, 64, 40, 8, 20, cam=scenes.MAIN_CAMERA,
+         what="main()'s defaults: pyramide_eau mesh at +-1813, camera main.c:300-301 (vfov 30.2, 16:10), "
+              "sun + radius-1e5 sky (main.c:345-346), 20 bounces"),
+    Case("main_regime_ao_b20", helpers.main_regime_scene, 48, 30, 8, 20, use_ao=True, ao=2.5,
+         cam=scenes.MAIN_CAMERA, what="main()'s regime + AO 2.5 (main.c:316-317 values), 20 bounces"),
+] + [Case("random_deep_%d" % s, _random(s, bounce_hi=25), 0, 0, 0, 0,
+          what="tests/test_gpu_fuzz.random_scene(%d, bounce_hi=25): 0-24 bounces" % s)
+     for s in (704, 705, 707, 708, 709, 712, 714, 717)]   # seeds drawing >= 12 bounces
 
 BY_NAME = {c.name: c for c in CASES}
 
@@ -188,21 +215,23 @@ class PhiloxCase:
     GPU takes (1: fixed grid; > 1: the persistent queue kernel)."""
 
     def __init__(self, name, build, W=64, H=48, spp=16, bounces=6, use_ao=False, ao=0.0, compat=1, chunks=32,
-                 seed=1010, what=""):
+                 seed=1010, what="", cam=None, kernel=None):
         self.name, self.build, self.W, self.H, self.spp, self.bounces = name, build, W, H, spp, bounces
         self.use_ao, self.ao, self.compat, self.chunks, self.seed, self.what = use_ao, ao, compat, chunks, seed, what
+        self.cam, self.kernel = cam, kernel      # kernel: rt_last_render_kernel() the GPU must take
 
     def scene(self):
         b = self.build()
         if isinstance(b, tuple):                 # random scene: its own params, Philox stream
             return b
         p = helpers.params(self.W, self.H, self.spp, self.bounces, use_ao=self.use_ao, ao=self.ao,
-                           seed=self.seed, compat=self.compat, chunks=self.chunks)
+                           seed=self.seed, compat=self.compat, chunks=self.chunks,
+                           cam=None if self.cam is None else helpers.camera_of(self.cam))
         return b, p
 
 
-def _random_philox(seed):
-    return _random(seed)
+def _random_philox(seed, bounce_hi=9):
+    return _random(seed, bounce_hi)
 
 
 PHILOX_CASES = [
@@ -220,7 +249,39 @@ PHILOX_CASES = [
     PhiloxCase("c4_tree_ao_2p5", helpers.tree_scene, W=40, H=30, spp=8, bounces=8, use_ao=True, ao=2.5,
                compat=0, chunks=1, what="C4 scene with AO 2.5 as a double, fixed-grid BVH kernel"),
 ] + [PhiloxCase("random_%d" % s, _random_philox(s), what="enclosed tests/test_gpu_fuzz.random_scene(%d)" % s)
-     for s in range(100, 116)]
+     for s in range(100, 116)] + [
+    # r06: 10 / 20 bounces (main.c:310), the nature scene, main()'s coordinate regime
+    PhiloxCase("glass_b20", _glass, bounces=20, chunks=4, what="translucent spheres, 20 bounces (QB -1)"),
+    PhiloxCase("glass_b20_fixed", _glass, W=48, H=36, bounces=20, chunks=1,
+               what="translucent spheres, 20 bounces, fixed grid"),
+    PhiloxCase("holes_ao_b20", _holes, bounces=20, use_ao=True, ao=2.0, chunks=3,
+               what="alpha-hole spheres + AO, 20 bounces"),
+    PhiloxCase("mineways_b10", helpers.mineways_scene, bounces=10, chunks=4, what="mineways, 10 bounces (QB 3)"),
+    PhiloxCase("mineways_b20", helpers.mineways_scene, W=48, H=36, bounces=20, chunks=32,
+               what="mineways, 20 bounces, spp_chunks 32"),
+    PhiloxCase("c4_tree_ao_b10", helpers.tree_scene, W=48, H=36, spp=8, bounces=10, use_ao=True, ao=2.5,
+               chunks=4, what="C4 tree + AO (int 2), 10 bounces, deep-tree opaque kernel"),
+    PhiloxCase("c4_tree_ao_b20", helpers.tree_scene, W=40, H=30, spp=8, bounces=20, use_ao=True, ao=2.5,
+               compat=0, chunks=8, kernel="render_kernel_q<QB=3,OP>", what="C4 tree + AO 2.5 (double), 20 bounces, deep-tree opaque kernel"),
+    PhiloxCase("nature_b10", helpers.nature_scene, W=48, H=36, spp=8, bounces=10, chunks=4,
+               cam=scenes.NATURE_CAMERA, kernel="render_kernel_q<QB=3>",
+               what="RTX_MAP/nature, 10 bounces: non-opaque deep-tree kernel (QB 3)"),
+    PhiloxCase("nature_b10_fixed", helpers.nature_scene, W=40, H=30, spp=4, bounces=10, chunks=1,
+               cam=scenes.NATURE_CAMERA, kernel="render_kernel<BVH>",
+               what="RTX_MAP/nature, 10 bounces, fixed-grid BVH kernel"),
+    PhiloxCase("nature_ao_b20", helpers.nature_scene, W=32, H=24, spp=8, bounces=20, use_ao=True, ao=2.5,
+               compat=0, chunks=8, cam=scenes.NATURE_CAMERA, kernel="render_kernel_q<QB=3>",
+               what="nature + AO 2.5, 20 bounces"),
+    PhiloxCase("main_regime_b20", helpers.main_regime_scene, W=64, H=40, spp=8, bounces=20, chunks=4,
+               cam=scenes.MAIN_CAMERA, kernel="render_kernel_q<QB=4>",
+               what="main()'s camera / mesh scale / radius-1e5 sky, 20 bounces (34 triangles: shallow BVH)"),
+    PhiloxCase("main_regime_ao_b20", helpers.main_regime_scene, W=48, H=30, spp=8, bounces=20, use_ao=True,
+               ao=2.5, compat=0, chunks=3, cam=scenes.MAIN_CAMERA, what="main()'s regime + AO 2.5, 20 bounces"),
+    PhiloxCase("main_regime_fixed", helpers.main_regime_scene, W=48, H=30, spp=4, bounces=20, chunks=1,
+               cam=scenes.MAIN_CAMERA, what="main()'s regime, 20 bounces, fixed grid"),
+] + [PhiloxCase("random_deep_%d" % s, _random_philox(s, bounce_hi=25),
+                what="enclosed tests/test_gpu_fuzz.random_scene(%d, bounce_hi=25)" % s)
+     for s in (722, 724, 726, 728, 730, 731, 732, 735)]   # seeds drawing >= 12 bounces
 
 PHILOX_BY_NAME = {c.name: c for c in PHILOX_CASES}
 

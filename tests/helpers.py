@@ -80,6 +80,26 @@ def tree_scene(move=scenes.TREE_MOVE):
     return SceneBundle(scenes.cornell_spheres(), scenes.moved(scenes.load_tree_fixture(), move))
 
 
+def camera_of(spec):
+    """scenes.*_CAMERA dict -> the oracle's init_camera (camera.h:21-40)."""
+    return oracle_ffi.oracle().oracle_init_camera(Vec3(*spec["origin"]), Vec3(*spec["target"]), Vec3(*spec["up"]),
+                                                  spec["vfov"], spec["ratio"])
+
+
+def nature_scene():
+    """RTX_MAP/nature (5812 textured triangles with alpha holes) lit by
+    main.c:345-346's sun and sky sphere; camera scenes.NATURE_CAMERA."""
+    return SceneBundle(scenes.main_spheres(), scenes.nature_mesh())
+
+
+def main_regime_scene():
+    """main()'s own coordinate regime: its default mesh pyramide_eau/scene.obj
+    (+-1813 units, materials 1/3/4 = texture.h:71-87's light / glass / water
+    overrides) under main.c:345-346's sun and radius-1e5 sky sphere; camera
+    scenes.MAIN_CAMERA (main.c:298-302)."""
+    return SceneBundle(scenes.main_spheres(), scenes.pyramide_eau_mesh())
+
+
 def params(W, H, spp, bounces, use_ao=False, ao=2.5, rng=RT_RNG_PHILOX, seed=1010, compat=1, cam=None,
            aperture=(0.0, 0.0), focus=3.0, chunks=1, accel=0, sky_mode=0, semantics=0):
     if cam is None:

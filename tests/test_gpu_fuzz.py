@@ -29,8 +29,13 @@ def _zero_some(rng, c, zeros):
     return tuple(0.0 if rng.random() < 0.35 else float(x) for x in c)
 
 
-def random_scene(seed, zeros=False, chunks=None, nt_range=None, spp=None, opaque=False, mesh_p=0.7):
-    """opaque: only opaque materials (no glass or hole spheres, texels at
+def random_scene(seed, zeros=False, chunks=None, nt_range=None, spp=None, opaque=False, mesh_p=0.7,
+                 bounce_hi=25, far=False):
+    """bounce_hi: nbRebondMax is drawn from [0, bounce_hi), covering main.c's
+    own default of 20 (main.c:310); the scenes pinned by reference fixtures
+    (tests/composition_cases._random) keep the r05 draw, bounce_hi 9.
+    far: the scene moved into main()'s coordinate regime (below).
+    opaque: only opaque materials (no glass or hole spheres, texels at
     alpha 1, no material index 3 or 4), the scenes the queue kernel's
     opaque instantiations take (QB -2, the deep-tree OPQ kernel);
     mesh_p: probability of a mesh when nt_range is None."""
@@ -75,14 +80,36 @@ def random_scene(seed, zeros=False, chunks=None, nt_range=None, spp=None, opaque
             mats[k] = scenes.material(_zero_some(rng, tuple(rng.uniform(0, 1, 3)), zeros), (0, 0, 0), 0.0, 0.0,
                                       1.0 if opaque else float(rng.choice([0.0, 0.5, 1.0, 0.7])), 0.0)
         mesh = (tris, qm, mats, tw, th, nm)
-    bundle = helpers.SceneBundle(sph, mesh)
-    cam = tipe_rt.init_camera(tuple(rng.uniform(-0.5, 0.5, 3)), tuple(rng.uniform([-1, -1, -4], [1, 1, -2])),
-                              (0, 1, 0), float(rng.uniform(40, 100)), 4.0 / 3.0)
+    cam_o, cam_t = rng.uniform(-0.5, 0.5, 3), rng.uniform([-1, -1, -4], [1, 1, -2])
+    vfov = float(rng.uniform(40, 100))
     W, H = int(rng.integers(8, 33)), int(rng.integers(6, 25))
-    p = helpers.params(W, H, int(rng.integers(1, 6)), int(rng.integers(0, 9)), use_ao=bool(rng.random() < 0.4),
-                       ao=float(rng.uniform(0.5, 3.5)), seed=int(rng.integers(0, 2 ** 40)), cam=cam,
-                       aperture=tuple(rng.choice([0.0, 0.0, 1.0, 2.0], 2)), focus=float(rng.uniform(1, 5)),
-                       compat=int(rng.integers(0, 2)), chunks=int(rng.choice([1, 1, 2, 3])))
+    spp_b = (int(rng.integers(1, 6)), int(rng.integers(0, bounce_hi)))
+    use_ao, ao, rseed = bool(rng.random() < 0.4), float(rng.uniform(0.5, 3.5)), int(rng.integers(0, 2 ** 40))
+    aperture, focus = tuple(rng.choice([0.0, 0.0, 1.0, 2.0], 2)), float(rng.uniform(1, 5))
+    compat, chunks_d = int(rng.integers(0, 2)), int(rng.choice([1, 1, 2, 3]))
+    if far:
+        # main()'s coordinate regime (camera at |o| ~ 1000, main.c:300-301;
+        # sky sphere of radius 1e5, main.c:346): the whole scene scaled by s
+        # and moved by T, then enclosed by an emissive radius-1e5 sky
+        s, T = float(rng.uniform(50, 2000)), rng.uniform(-1000, 1000, 3)
+        for k in range(ns):
+            sph[k].center = Vec3(*(T + s * np.array(sph[k].center.tolist())))
+            sph[k].radius = s * sph[k].radius
+        if mesh is not None:
+            for t in mesh[0]:
+                t.A, t.B, t.C = (Vec3(*(T + s * np.array(P.tolist()))) for P in (t.A, t.B, t.C))
+        cam_o, cam_t = T + s * cam_o, T + s * cam_t
+        focus *= s
+        sky = (Sphere * (ns + 1))()
+        for k in range(ns):
+            sky[k] = sph[k]
+        sky[ns].center, sky[ns].radius = Vec3(0.0, 0.0, 0.0), 1e5
+        sky[ns].mat = scenes.material((0, 0, 0), scenes.SKY, 1.0, 0.0, 1.0, 1.0)
+        sph = sky
+    bundle = helpers.SceneBundle(sph, mesh)
+    cam = tipe_rt.init_camera(tuple(cam_o), tuple(cam_t), (0, 1, 0), vfov, 4.0 / 3.0)
+    p = helpers.params(W, H, *spp_b, use_ao=use_ao, ao=ao, seed=rseed, cam=cam, aperture=aperture, focus=focus,
+                       compat=compat, chunks=chunks_d)
     if chunks is not None:
         p.spp_chunks = chunks
         p.nbRayonParPixel = max(p.nbRayonParPixel, chunks)
@@ -94,6 +121,17 @@ def random_scene(seed, zeros=False, chunks=None, nt_range=None, spp=None, opaque
 @pytest.mark.parametrize("seed", range(64))
 def test_random_scene_bitexact(seed):
     bundle, p = random_scene(seed)
+    check_parity(bundle, p)
+
+
+@pytest.mark.parametrize("seed", range(800, 840))
+def test_random_far_scene_bitexact(seed):
+    """main()'s coordinate regime: every random scene scaled by 50-2000 and
+    moved by up to 1000 units, inside a radius-1e5 emissive sky sphere
+    (main.c:300-301, 346), so the candidate pass's interval bound
+    (Hs = (|o| + L) sqrt(a)) and the BVH padding run at |o|, L ~ 1e3-1e5;
+    0-24 bounces; spp_chunks 1-3; bit for bit vs the oracle."""
+    bundle, p = random_scene(seed, far=True)
     check_parity(bundle, p)
 
 

@@ -97,7 +97,7 @@ def test_tree_with_override_material_keeps_qb3(mat_index):
     assert render_and_compare(bundle, p) == "render_kernel_q<QB=3>"
 
 
-@pytest.mark.parametrize("scene", ["tree", "sweep", "mineways"])
+@pytest.mark.parametrize("scene", ["tree", "sweep", "mineways", "nature", "main_regime"])
 def test_bvh_stack_bound_holds_on_the_gpu(scene):
     """rt_count_async checks every BVH push against the LDS stack of the
     kernel launch_render picks for the tree (rt.h RT_CNT_BVH_STACK_OVER):
@@ -108,6 +108,13 @@ def test_bvh_stack_bound_holds_on_the_gpu(scene):
         bundle = helpers.tree_scene()
     elif scene == "mineways":
         bundle = helpers.mineways_scene()
+    elif scene in ("nature", "main_regime"):       # 5812 triangles, stack4 22 / main()'s scale
+        bundle = helpers.nature_scene() if scene == "nature" else helpers.main_regime_scene()
+        p = helpers.params(120, 90, 4, 10, use_ao=True, ao=2.5, chunks=4,
+                           cam=helpers.camera_of(scenes.NATURE_CAMERA if scene == "nature" else scenes.MAIN_CAMERA))
+        c = assert_stack_bound_holds(bundle, p)
+        assert c[tipe_rt.types.RT_CNT_BVH_NODES] > 0
+        return
     else:
         sph, mesh = scenes.synthetic_cornell(10, 100)
         bundle = helpers.SceneBundle(sph, mesh)

@@ -63,6 +63,10 @@ def test_gpu_matches_reference_code(name):
     bundle, p = _scene(name)
     canva, alb, nrm, rad = gpu_render(bundle, p)
     _check(name, dict(canva=canva, albedo=alb, normal=nrm, radiance=rad))
+    want = cc.PHILOX_BY_NAME[name].kernel
+    if want is not None:
+        import tipe_rt
+        assert tipe_rt.last_render_kernel() == want
 
 
 @pytest.mark.parametrize("name", NAMES)

@@ -73,12 +73,20 @@ def load_mesh_fixture(name):
     Returns (triangles, quelMatPourTri, mat_list, tw, th, n_materials)."""
     with open(os.path.join(_GOLDEN, "scenes", name + ".json")) as f:
         d = json.load(f)
-    tris = d["triangles"]
-    arr = (Triangle * len(tris))()
-    for k, t in enumerate(tris):
-        arr[k].A, arr[k].B, arr[k].C = Vec3(*t["A"]), Vec3(*t["B"]), Vec3(*t["C"])
-        arr[k].uvA, arr[k].uvB, arr[k].uvC = UV(*t["uvA"]), UV(*t["uvB"]), UV(*t["uvC"])
-        arr[k].mat = material(SKY, BLACK, 0.0, 0.0, 0.0, 0.0)   # mesh.h:206
+    if "tri" in d:          # compact rows (tests/golden/make_scene_fixtures.py)
+        tris = d["tri"]
+        arr = (Triangle * len(tris))()
+        for k, t in enumerate(tris):
+            arr[k].A, arr[k].B, arr[k].C = Vec3(*t[0:3]), Vec3(*t[3:6]), Vec3(*t[6:9])
+            arr[k].uvA, arr[k].uvB, arr[k].uvC = UV(*t[9:11]), UV(*t[11:13]), UV(*t[13:15])
+            arr[k].mat = material(SKY, BLACK, 0.0, 0.0, 0.0, 0.0)   # mesh.h:206
+    else:
+        tris = d["triangles"]
+        arr = (Triangle * len(tris))()
+        for k, t in enumerate(tris):
+            arr[k].A, arr[k].B, arr[k].C = Vec3(*t["A"]), Vec3(*t["B"]), Vec3(*t["C"])
+            arr[k].uvA, arr[k].uvB, arr[k].uvC = UV(*t["uvA"]), UV(*t["uvB"]), UV(*t["uvC"])
+            arr[k].mat = material(SKY, BLACK, 0.0, 0.0, 0.0, 0.0)   # mesh.h:206
     qm = (C.c_int * len(tris))(*d["quelMatPourTri"])
     tex = d["texels"]
     mats = (Material * len(tex))()
@@ -122,6 +130,45 @@ def load_tree_fixture():
     for k, (r, g, b, a, refl) in enumerate(d["texels"]):
         mats[k] = material((r, g, b), BLACK, 0.0, refl, a, 0.0)
     return arr, qm, mats, d["tex_width"], d["tex_height"], d["n_materials"]
+
+
+# main()'s own settings (main.c:293-346): its camera at the +-1813 scale of
+# its default mesh model3D/pyramide_eau/scene.obj, and the two last entries
+# of its sphere list -- the sun (main.c:345) and the sky sphere of radius
+# 1e5 (main.c:346, "derniere sphère = ciel").
+MAIN_CAMERA = dict(origin=(237.6461, 144.496, -962.8788), target=(-176.9382, 141.5864, 651.8203), up=(0, 1, 0),
+                   vfov=30.2, ratio=16.0 / 10.0)
+MAIN_SUN = ((0.5145, 2.7877, -1.1792), 0.1, BLACK, WHITE, 70.0, 0.0)
+MAIN_SKY = ((0.0, 0.0, 0.0), 100000.0, BLACK, SKY, 1.0, 0.0)
+# RTX_MAP/nature (the reference's RTX_nature_1000RAYS_9RB render): a camera
+# low in the valley looking across the pond, as the scene's screenshot
+# (model3D/RTX_MAP/nature/screen/); chosen here, the reference's own is not
+# recorded.  The mesh is used where the loader leaves it (move_mesh(0, 0, 0),
+# main.c:366).
+NATURE_CAMERA = dict(origin=(1.0, 0.6, 1.3), target=(-0.6, 0.75, -0.9), up=(0, 1, 0), vfov=60.0, ratio=4.0 / 3.0)
+
+
+def main_spheres():
+    """main.c:345-346: sun + sky sphere (radius 1e5), the sky last."""
+    arr = (Sphere * 2)()
+    for k, (c, r, d, e, es, rf) in enumerate((MAIN_SUN, MAIN_SKY)):
+        arr[k].center = Vec3(*c)
+        arr[k].radius = r
+        arr[k].mat = material(d, e, es, rf, 1.0, 1.0)
+    return arr
+
+
+def nature_mesh():
+    """model3D/RTX_MAP/nature/mineways_doubleface_tri.obj through the
+    reference loader (tests/golden/scenes/nature.json): 5812 triangles, 31
+    16x16 textures with alpha."""
+    return load_mesh_fixture("nature")
+
+
+def pyramide_eau_mesh():
+    """main()'s default mesh (main.c:320) through the reference loader,
+    synthetic texels (its PPMs are missing blobs)."""
+    return load_mesh_fixture("pyramide_eau")
 
 
 def pyramid_mesh():
