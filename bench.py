@@ -169,10 +169,20 @@ CONFIGS = {
     "C4": ("tree", 2000, 8, True, 1200, 900, 2000, 4),
     "C5": ("pyramid", 5000, 6, False, 3840, 2880, 5000, 8),
     "sweep_10s_100t": ("sweep", 64, 6, False, 1200, 900, 64, 1),
+    # the reference's own production scene (RTX_MAP/nature, 5812 textured triangles with
+    # alpha holes, lit by main.c:345-346's sun and radius-1e5 sky) at its own render
+    # settings: 1000 rays, nbRebondMax 10 (RTX_nature_1000RAYS_9RB, .MISSING_LARGE_BLOBS:8,
+    # name rule main.c:328); 1200x900 as the other configs; camera scenes.NATURE_CAMERA
+    "nature": ("nature", 1000, 10, False, 1200, 900, 1000, 1),
 }
+CONFIG_CAMERA = {"nature": scenes.NATURE_CAMERA}
 
 
 def config_scene(kind):
+    if kind == "nature":
+        sph = scenes.main_spheres()
+        tris, qm, mats, tw, th, nm = scenes.nature_mesh()
+        return tipe_rt.make_scene(sph, tris, qm, mats, tw, th, nm), len(sph), len(tris)
     sph = scenes.cornell_spheres()
     if kind == "pyramid":
         return tipe_rt.make_scene(sph, *scenes.pyramid_mesh()), len(sph), 5
@@ -204,11 +214,18 @@ def task_regime(spp, w, h):
             "tasks": w * h * P}
 
 
-def configs_extra(dev, stream, cam):
+def config_camera(name, cam):
+    spec = CONFIG_CAMERA.get(name)
+    return cam if spec is None else tipe_rt.init_camera(**{k: spec[k] for k in ("origin", "target", "up", "vfov",
+                                                                                 "ratio")})
+
+
+def configs_extra(dev, stream, cam0):
     out = {}
     sptr = stream.cuda_stream
     for name, (kind, spp, bounces, ao, w, h, full_spp, gpus) in CONFIGS.items():
         sc, ns, nt = config_scene(kind)
+        cam = config_camera(name, cam0)
         p = tipe_rt.make_params(w, h, spp, bounces, cam, focus=3.0, use_ao=ao, ao=2.5, seed=SEED,
                                 chunks=tipe_rt.RT_SPP_CHUNKS_AUTO)
         ds = tipe_rt.DeviceScene(sc, dev.index)
@@ -235,6 +252,7 @@ def configs_extra(dev, stream, cam):
         ev[1].record(stream)
         torch.cuda.synchronize(dev)
         ms = ev[0].elapsed_time(ev[1]) / reps
+        kname = tipe_rt.last_render_kernel()
         pc = tipe_rt.make_params(w, h, 2, bounces, cam, focus=3.0, use_ao=ao, ao=2.5, seed=SEED)
         d = torch.zeros(tipe_rt.RT_NCOUNTERS, dtype=torch.int64, device=dev)
         tipe_rt.count_async(ds, pc, tiling, d.data_ptr(), sptr)
@@ -251,10 +269,22 @@ def configs_extra(dev, stream, cam):
                "flops_per_sample_work_done": round(fps, 1), "achieved_tflops": round(tf, 3),
                "frac": round(tf / FP64_VECTOR_PEAK_TFLOPS, 4),
                "casts_per_sample": round(c[T.RT_CNT_CASTS] / max(c[0], 1), 3)}
+        if ao:
+            # make_params' default compat_int_truncation = 1: ThreadData's int AO_intensity
+            # (main.c:43) turns the requested 2.5 into 2, as the reference's fill_canva does
+            rec["ao_intensity"] = 2.5
+            rec["ao_intensity_effective"] = float(int(2.5)) if p.compat_int_truncation else 2.5
+        rec["kernel"] = kname
         if c[T.RT_CNT_BVH_NODES]:
             rec["bvh_nodes_per_sample"] = round(c[T.RT_CNT_BVH_NODES] / c[0], 3)
             rec["bvh_tri_tests_per_sample"] = round(c[T.RT_CNT_BVH_TRI_TESTS] / c[0], 3)
             rec["bvh_simd_efficiency"] = round(c[T.RT_CNT_BVH_NODES] / max(c[T.RT_CNT_BVH_LANE_SLOTS], 1), 4)
+            # with a BVH the brute-force F (every cast tests all N_t triangles,
+            # main.c:81-90) is reported beside the work-done figure; its "frac" exceeds 1 by
+            # what the tree saves
+            fref = flops_per_launch(c, ns, nt) / max(c[0], 1)
+            rec["flops_per_sample_reference"] = round(fref, 1)
+            rec["frac_reference_bruteforce"] = round(rate * 1e6 * fref / 1e12 / FP64_VECTOR_PEAK_TFLOPS, 4)
         if kind != "sweep":
             rec["full_frame_s_1gpu"] = round(ms * 1e-3 * full_spp / spp, 3)
             rec["config_gpus"] = gpus
@@ -284,10 +314,12 @@ def configs_sharded(args, rank, world, dev, cam, names):
     out = {}
     gpu = dev.index
     st = torch.cuda.current_stream(dev)
+    cam0 = cam
     for name in names:
         kind, _, bounces, ao, w, h, full_spp, gpus = CONFIGS[name]
         spp = args.config_spp or full_spp
         sc, ns, nt = config_scene(kind)
+        cam = config_camera(name, cam0)
         ds = tipe_rt.DeviceScene(sc, gpu)
         tiling = tipe_rt.cyclic_tiling(h, TILE_ROWS, rank, world)
         rows = tiling.n_tiles * TILE_ROWS
@@ -356,6 +388,8 @@ def configs_sharded(args, rank, world, dev, cam, names):
                "rows_per_rank": rows, "frames_timed": 1, "warmup_spp": warm.nbRayonParPixel,
                "collective": "rccl gather" if args.dist_backend == "nccl" else "gloo gather (host)",
                "gather_payload": "canva as float32, 12 B/px", "scaling": "strong"}
+        if ao:
+            rec["ao_intensity_effective"] = float(int(2.5)) if p.compat_int_truncation else 2.5
         if args.verify and rank == 0:
             ref = torch.empty((h, w, 3), dtype=torch.float64, device=dev)
             tipe_rt.render_async(ds, p, tipe_rt.band_tiling(0, h - 1), ref.data_ptr(), stream=st.cuda_stream)
@@ -548,7 +582,7 @@ def main():
                     help="N>1: skip the single_process leg (rt_render_gather_async over the N devices)")
     ap.add_argument("--configs", default="C3,C4,C5",
                     help="N>1: BASELINE configs rendered row-tiled over the N ranks after the C2 headline "
-                         "(comma list of C3, C4, C5; empty: none)")
+                         "(comma list of C3, C4, C5, nature; empty: none)")
     ap.add_argument("--config-spp", type=int, default=0,
                     help="N>1 config legs: render at this spp instead of each config's full spp (tests)")
     args = ap.parse_args()
@@ -691,7 +725,7 @@ def main():
     sharded = None
     if world > 1 and args.configs:
         names = [n.strip() for n in args.configs.split(",") if n.strip()]
-        bad = [n for n in names if n not in ("C3", "C4", "C5")]
+        bad = [n for n in names if n not in ("C3", "C4", "C5", "nature")]
         if bad:
             raise SystemExit("bench.py: unknown --configs %s" % bad)
         sharded = configs_sharded(args, rank, world, dev, cam, names)
@@ -765,6 +799,9 @@ def main():
                                                "is the last committed rocprofv3 PMC value (traffic_source)",
                          "kernel": "render_kernel_q<false, 0, -2, false> (persistent task queue, sphere-only opaque-material instantiation; no sky, no AO, no BVH) + combine_kernel",
                          "kernel_ms": round(kernel_ms, 3), "flops_per_launch": flops,
+                         "scope": "whole frame (1 GPU)" if world == 1 else
+                                  "per rank: rank 0's cyclic row tiles (%d of %d rows), its own kernel time"
+                                  % (valid_rows(tiling), H),
                          "flops_per_sample": round(flops / launch_samples, 1),
                          "note": "achieved = algorithmic FLOPs of the work done (SURVEY 8d formula on the "
                                  "kernel's own event counts; paths end at zero throughput) / kernel time",

@@ -195,5 +195,5 @@ def test_random_opaque_bvh_scene_queue_bitexact(seed, monkeypatch):
     assert_stack_bound_holds(bundle, p)
     # deep trees take the OPQ kernel; shallow ones QB 4; a camera outside the
     # scene bound the brute-force scan (QB 0); an over-deep tree the fixed grid
-    assert tipe_rt.last_render_kernel() in ("render_kernel_q<QB=3,OP>", "render_kernel_q<QB=4>",
+    assert tipe_rt.last_render_kernel() in ("render_kernel_q<QB=3,OP>", "render_kernel_q<QB=3>", "render_kernel_q<QB=4>",
                                             "render_kernel_q<QB=0>", "render_kernel<BVH>")

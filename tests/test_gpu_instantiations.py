@@ -121,3 +121,30 @@ def test_bvh_stack_bound_holds_on_the_gpu(scene):
     p = helpers.params(120, 90, 4, 8, use_ao=True, ao=2.5, chunks=4)
     c = assert_stack_bound_holds(bundle, p)
     assert c[tipe_rt.types.RT_CNT_BVH_NODES] > 0          # the tree was walked
+
+
+def _nature(opaque):
+    tris, qm, mats, tw, th, nm = scenes.nature_mesh()
+    if opaque:                          # every texel at alpha 1, no material index 3 / 4 override
+        for k in range(len(mats)):
+            mats[k].alpha = 1.0
+        for k in range(len(tris)):
+            if qm[k] in (3, 4):
+                qm[k] = 0
+    return helpers.SceneBundle(scenes.main_spheres(), (tris, qm, mats, tw, th, nm))
+
+
+@pytest.mark.parametrize("opaque", [False, True])
+def test_tree_with_stack_bound_above_24_keeps_the_queue_kernel(opaque):
+    """RTX_MAP/nature under main.c:346's radius-1e5 sky: the scene radius
+    (1e5) widens every triangle's padding (rt_bvh.cpp), and the tree's exact
+    stack bound becomes 25 > 24.  The non-opaque deep-tree kernel has 32 LDS
+    stack entries (kStackQN; 38 KiB per block, still 4 blocks per CU), so it
+    takes such trees -- an opaque one too, instead of the 24-entry OPQ
+    kernel -- rather than the fixed grid; every push stays inside
+    (RT_CNT_BVH_STACK_OVER == 0), bit for bit vs the oracle."""
+    from test_gpu_parity import assert_stack_bound_holds
+    bundle = _nature(opaque)
+    p = helpers.params(32, 24, 4, 10, chunks=4, cam=helpers.camera_of(scenes.NATURE_CAMERA))
+    assert render_and_compare(bundle, p) == "render_kernel_q<QB=3>"
+    assert_stack_bound_holds(bundle, p)

@@ -473,9 +473,20 @@ int launch_on_stream(KParams& kp, const double* uni, hipStream_t st, bool count)
     kp.uni = d_uni;
     kp.partial = d_part;
     // the queue kernel numbers tasks (chunk, pixel of the band) in 32 bits
-    // the queue kernel numbers tasks (chunk, pixel of the band) in 32 bits
     kp.task_ctr = (d_part && (unsigned long long)band * kp.W * kp.chunks < (1ull << 31))
                       ? (unsigned*)(d_uni + ((U_COUNT + 7) / 8 + 1) * 8) : nullptr;
+    // the stack of the kernel a render of these params takes (a count run emulates
+    // the render's banding to find out whether that render has the task counter)
+    {
+        int band_r = kp.local_rows;
+        if (kp.chunks > 1) {
+            const size_t per_row = (size_t)kp.chunks * kp.W * 9 * sizeof(double);
+            band_r = (int)std::min<size_t>(std::max<size_t>(16, partial_budget() / per_row / 16 * 16),
+                                           (size_t)kp.local_rows);
+        }
+        const bool task_ok = kp.chunks > 1 && (unsigned long long)band_r * kp.W * kp.chunks < (1ull << 31);
+        kp.stack_cap = choose_render(kp, count ? task_ok : kp.task_ctr != nullptr).stack_cap;
+    }
     for (int y0 = 0; e == hipSuccess && y0 < kp.local_rows; y0 += band) {
         kp.band_y0 = y0;
         kp.band_rows = band;

@@ -148,7 +148,19 @@ struct KParams {
     int ns_cand;             // spheres the candidate pass scans: ns_pad, or 0 when cand_lmax is +inf (every
                              // ray then takes the exact scan: non-finite spheres, or more than 65534
                              // spheres, whose slots do not fit RT_CAND_TAG's 16 bits)
+    int stack_cap;           // BVH stack entries of the kernel launch_render picks for this launch
+                             // (choose_render; host-set): what COUNT runs check pushes against
 };
+
+// The render kernel launch_render takes and its BVH walk's LDS stack entries
+// (rt_kernels.hip choose_render).
+struct RenderChoice {
+    bool queue;              // render_kernel_q (else the fixed-grid render_kernel / render_kernel_cuda)
+    int qb;                  // render_kernel_q's QB
+    bool opq;                // ... its OPQ instantiation
+    int stack_cap;           // stack entries of the chosen kernel's BVH walk (0 without a BVH)
+};
+RenderChoice choose_render(const KParams& kp, bool task_ok);
 
 struct UniBlock { double v[U_COUNT]; };
 

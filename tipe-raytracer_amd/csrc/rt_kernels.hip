@@ -656,29 +656,22 @@ __device__ __forceinline__ unsigned short* bvh_stack()
     __shared__ unsigned short stk_lds[kStack4 * 256];
     return stk_lds + threadIdx.x;
 }
-// The queue kernel's per-lane stack (BVH scenes): [kStackQ][256] uint16, 12 KiB,
-// which keeps the kernel at 4 blocks (16 waves) per CU; trees that could need
-// more entries (kp.bvh_stack > kStackQ) render with the fixed-grid kernel.
-// The QB = 4 instantiation (shallow trees: bvh_steps 4, i.e. depth4 <= 4) is
-// admitted only when the tree's exact stack bound (rt_bvh.cpp stack4) is at
-// most kStackQ4 = 14 entries, so its top-node cache and the task table fit the
-// same 40 KiB; deeper or wider trees take QB = 3 (kStackQ) or the fixed grid
-// (stack_cap_of below; RT_CNT_BVH_STACK_OVER checks the bound on the GPU).
-constexpr int kStackQ = 24, kStackQ4 = 14;
-// The LDS stack entries of the kernel launch_render picks for a tree: the
-// queue kernel's QB = 4 (kStackQ4) or QB = 3 (kStackQ) instantiation, else
-// the fixed-grid kernel (kStack4).  COUNT runs check every push against it
-// (RT_CNT_BVH_STACK_OVER), so a host stack bound that misses the kernel's
-// push rule shows up as a count, not as a neighbour lane's corrupted stack.
-__host__ __device__ inline int stack_cap_of(int bvh_stack, int bvh_steps)
-{
-    if (bvh_stack > kStackQ) return kStack4;
-    return bvh_steps <= 3 || bvh_stack > kStackQ4 ? kStackQ : kStackQ4;
-}
-template <int QB>
+// The queue kernel's per-lane stack (BVH scenes): uint16 [entries][256].  The
+// deep-tree instantiations (QB = 3) get kStackQ = 24 entries (12 KiB) when every
+// material is opaque (OPQ: incomingLight also lives in LDS) and kStackQN = 32
+// (16 KiB) otherwise, which keeps both at <= 40 KiB, i.e. 4 blocks (16 waves) per
+// CU.  The QB = 4 instantiation (shallow trees: bvh_steps 4, i.e. depth4 <= 4) is
+// admitted only when the tree's exact stack bound (rt_bvh.cpp stack4) is at most
+// kStackQ4 = 14 entries, so its top-node cache and the task table fit the same
+// 40 KiB.  An opaque tree whose bound lies in (24, 32] takes the non-OPQ QB = 3
+// kernel; a bound above 32 the fixed grid (kStack4).  choose_render below is the
+// one place that decides; the host stores its stack in KParams::stack_cap, which
+// the COUNT runs check every push against (RT_CNT_BVH_STACK_OVER).
+constexpr int kStackQ = 24, kStackQN = 32, kStackQ4 = 14;
+template <int QB, bool OPQ>
 __device__ __forceinline__ unsigned short* bvh_stack_q()
 {
-    __shared__ unsigned short stkq_lds[(QB == 4 ? kStackQ4 : kStackQ) * 256];
+    __shared__ unsigned short stkq_lds[(QB == 4 ? kStackQ4 : OPQ ? kStackQ : kStackQN) * 256];
     return stkq_lds + threadIdx.x;
 }
 // ... and the block's copy of the tree's top nodes (RT_QB_TOP x 128 B, or
@@ -885,7 +878,7 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
                 next = ch;
                 tnext = tn[c];
             }
-            if (COUNT && sp >= stack_cap_of(kp.bvh_stack, kp.bvh_steps)) cnt.c[RT_CNT_BVH_STACK_OVER] += 1;
+            if (COUNT && sp >= kp.stack_cap) cnt.c[RT_CNT_BVH_STACK_OVER] += 1;
             if (!COUNT || sp < kStack4) {    // COUNT walks use the fixed grid's stack
                 stk[sp * 256] = (unsigned short)push;
                 ++sp;
@@ -1761,7 +1754,7 @@ __device__ __forceinline__ bool coop_step(const KParams& kp, const V3 o, const V
                 push[npush] = (unsigned)pu;
                 ++npush;
             } else {
-                if (COUNT && sp >= stack_cap_of(kp.bvh_stack, kp.bvh_steps)) cnt.c[RT_CNT_BVH_STACK_OVER] += 1;
+                if (COUNT && sp >= kp.stack_cap) cnt.c[RT_CNT_BVH_STACK_OVER] += 1;
                 if (!COUNT || sp < kStack4) {
                     stk[sp * 256] = (unsigned short)pu;
                     ++sp;
@@ -2509,7 +2502,7 @@ void render_kernel_q(const KParams kp)
 #endif
                 const V3 dd = L.cast_dir();
                 const Ray32 r32 = ray32(L.o, dd, kp.bvh_rbox);
-                unsigned short* stk = bvh_stack_q<QB>();
+                unsigned short* stk = bvh_stack_q<QB, OPQ>();
                 const QNode* top = NTOP > 0 ? bvh_top_q<QNode, NTOP>() : nullptr;
 #pragma unroll 1
                 for (int j = 0; j < QB; ++j) {
@@ -3045,27 +3038,48 @@ static unsigned qdiv_magic(unsigned d) { return d ? (unsigned)(0xffffffffull / d
 static thread_local const char* t_last_kernel = "none";
 const char* last_render_kernel() { return t_last_kernel; }
 
+// Which render kernel a launch takes (launch_render) and the LDS stack entries
+// that kernel gives a BVH walk.  task_ok: the launch has render_kernel_q's task
+// counter (spp_chunks > 1 and the band's tasks fit 32 bits, launch_on_stream).
+// Node visits per lane and round: 4 for shallow trees (128-byte nodes, kp.bvh),
+// 3 for deep ones (kp.bvh_steps, host; compile-time per instantiation).  The
+// deep-tree instantiation walks the 64-byte nodes kp.bvhh: a deep tree that
+// pack_bvh_h refused (a coordinate beyond binary16's range, a leaf index above
+// 65535, an oversized leaf) renders with the fixed-grid kernel; a shallow one
+// keeps the queue kernel.
+RenderChoice choose_render(const KParams& kp, bool task_ok)
+{
+    RenderChoice c;
+    c.queue = false;
+    c.qb = 0;
+    c.opq = false;
+    c.stack_cap = kp.bvh ? kStack4 : 0;
+#if RT_QUEUE > 0
+    bool qbvh = false;
+    if (kp.bvh != nullptr && kp.bvh_stack <= kStackQN) {
+        c.qb = kp.bvh_steps <= 3 || kp.bvh_stack > kStackQ4 ? 3 : 4;
+        qbvh = c.qb == 4 || !RT_QNODE_H || kp.bvhh != nullptr;
+    }
+    if (task_ok && kp.chunks > 1 && (!kp.bvh || qbvh) && !kp.cuda && !kp.sums) {
+        c.queue = true;
+        if (!qbvh) c.qb = RT_QSPHERES && kp.nt == 0 ? (RT_QOPAQUE && kp.opaque ? -2 : -1) : 0;
+        c.opq = RT_QOPAQUE_BVH && c.qb == 3 && kp.opaque_all && kp.bvh_stack <= kStackQ;
+        if (kp.bvh) c.stack_cap = c.qb == 4 ? kStackQ4 : c.opq ? kStackQ : kStackQN;
+    }
+#endif
+    return c;
+}
+
 int launch_render(const KParams& kp, void* stream)
 {
+    const RenderChoice rc = choose_render(kp, kp.task_ctr != nullptr);
 #if RT_QUEUE > 0
-    // Node visits per lane and round: 4 for shallow trees (128-byte nodes,
-    // kp.bvh), 3 for deep ones (kp.bvh_steps, host; compile-time per
-    // instantiation).  The deep-tree instantiation walks the 64-byte nodes
-    // kp.bvhh: a deep tree that pack_bvh_h refused (a coordinate beyond
-    // binary16's range, a leaf index above 65535, an oversized leaf) renders
-    // with the fixed-grid kernel; a shallow one keeps the queue kernel.
-    int qb = 0;
-    bool qbvh = false;
-    if (kp.bvh != nullptr && kp.bvh_stack <= kStackQ) {
-        qb = stack_cap_of(kp.bvh_stack, kp.bvh_steps) == kStackQ ? 3 : 4;
-        qbvh = qb == 4 || !RT_QNODE_H || kp.bvhh != nullptr;
-    }
-    if (kp.task_ctr && kp.chunks > 1 && (!kp.bvh || qbvh) && !kp.cuda && !kp.sums) {
+    if (rc.queue) {
         const hipStream_t st = (hipStream_t)stream;
         const bool sky = kp.sky != nullptr, ao = kp.useAO != 0;
         (void)hipMemsetAsync(kp.task_ctr, 0, sizeof(unsigned), st);
-        if (!qbvh) qb = RT_QSPHERES && kp.nt == 0 ? (RT_QOPAQUE && kp.opaque ? -2 : -1) : 0;
-        const bool opq = RT_QOPAQUE_BVH && qb == 3 && kp.opaque_all;
+        const int qb = rc.qb;
+        const bool opq = rc.opq;
         t_last_kernel = qb == 3   ? (opq ? "render_kernel_q<QB=3,OP>" : "render_kernel_q<QB=3>")
                         : qb == 4 ? "render_kernel_q<QB=4>"
                         : qb == -2 ? "render_kernel_q<QB=-2>"

@@ -36,13 +36,15 @@ CONFIGS = {
     "C5": (scenes.pyramid_mesh, 20, 6, False, 2.5, 5000, 3840, 2880, 8),
     # roofline-sweep scene: README box + 10 random spheres... (synthetic_cornell(10, 100))
     "SWEEP": ("sweep", 32, 6, False, 2.5, 32, 1200, 900, 1),
+    # the reference's RTX_MAP/nature scene at its own settings (1000 rays, nbRebondMax 10)
+    "NATURE": (scenes.nature_mesh, 64, 10, False, 2.5, 1000, 1200, 900, 1),
 }
 
 
 def run(name, spp_scale, dev, stream, spp_override=0, chunks=None):
     mesh_fn, spp, bounces, ao, ao_int, full_spp, W, H, gpus = CONFIGS[name]
     spp = spp_override or max(1, int(spp * spp_scale))
-    spheres = scenes.cornell_spheres()
+    spheres = scenes.main_spheres() if name == "NATURE" else scenes.cornell_spheres()
     if mesh_fn == "sweep":
         spheres, (tris, qm, mats, tw, th, nm) = scenes.synthetic_cornell(10, 100)
         scene = tipe_rt.make_scene(spheres, tris, qm, mats, tw, th, nm)
@@ -54,7 +56,8 @@ def run(name, spp_scale, dev, stream, spp_override=0, chunks=None):
         tris, qm, mats, tw, th, nm = mesh_fn()
         scene = tipe_rt.make_scene(spheres, tris, qm, mats, tw, th, nm)
         nt = len(tris)
-    cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
+    spec = scenes.NATURE_CAMERA if name == "NATURE" else scenes.README_CAMERA
+    cam = tipe_rt.init_camera(**{k: spec[k] for k in ("origin", "target", "up", "vfov", "ratio")})
     p = tipe_rt.make_params(W, H, spp, bounces, cam, focus=3.0, use_ao=ao, ao=ao_int,
                             chunks=tipe_rt.RT_SPP_CHUNKS_AUTO if chunks is None else chunks)
     ds = tipe_rt.DeviceScene(scene, dev.index)
@@ -77,6 +80,7 @@ def run(name, spp_scale, dev, stream, spp_override=0, chunks=None):
     torch.cuda.synchronize(dev)
     wall = (time.perf_counter() - t0) / n
     ms = ev[0].elapsed_time(ev[1]) / n
+    kname = tipe_rt.last_render_kernel()
     pc = tipe_rt.make_params(W, H, 4, bounces, cam, focus=3.0, use_ao=ao, ao=ao_int)
     d_cnt = torch.zeros(tipe_rt.RT_NCOUNTERS, dtype=torch.int64, device=dev)
     tipe_rt.count_async(ds, pc, tiling, d_cnt.data_ptr(), sptr)
@@ -85,7 +89,7 @@ def run(name, spp_scale, dev, stream, spp_override=0, chunks=None):
     ds.close()
     samples = W * H * spp
     rate = samples / (ms * 1e-3) / 1e6
-    return {"config": name, "width": W, "height": H, "triangles": nt, "spheres": len(spheres), "bounces": bounces,
+    return {"config": name, "kernel": kname, "width": W, "height": H, "triangles": nt, "spheres": len(spheres), "bounces": bounces,
             "ao": ao, "spp_measured": spp, "kernel_ms": round(ms, 3), "wall_ms": round(wall * 1e3, 3),
             "kernel_msamples_per_s": round(rate, 3),
             "full_frame_s_at_config_spp": round(W * H * full_spp / (rate * 1e6), 2),
