@@ -22,7 +22,8 @@ row-tiled over the same N ranks with the same RCCL gather (configs_sharded:
 Msamples/s, ms per frame, gather ms, per-rank render spread).  At N > 1 rank
 0 also times `single_process`: the
 library's own one-process multi-device frame (rt_render_gather_async over
-the N devices, peer copies over xGMI), the path a C caller of rt.h uses.
+the N devices, its own RCCL ncclGather over xGMI), the path a C caller of
+rt.h uses.
 
 Rank 0 prints ONE JSON line.  Besides the C2 headline it carries (N = 1,
 rank 0): `configs` (C3, C4, C5 and the 10-sphere/100-triangle sweep scene at
@@ -530,10 +531,17 @@ def single_process_leg(scene, p, world, devs, steps, verify_ref=None):
     """§8(e)'s in-library path for a C caller: one process, rt_init over the N
     devices, rt_render_gather_async per frame (every device renders its cyclic
     1-row tiles on a pooled stream, the canva planes travel to the first
-    device by peer copies over xGMI and are assembled there).  Timed over
-    `steps` frames after one warm-up frame; canva only, as the bench's gather."""
+    device by the library's RCCL ncclGather over xGMI -- peer copies when a
+    rehearsal repeats a device -- and are assembled there; `transport` names
+    the one used).  Timed over `steps` frames after one warm-up frame; canva
+    only, as the bench's gather."""
     L = tipe_rt.lib()
     tipe_rt.check(L.rt_init(len(devs), (C.c_int * len(devs))(*devs)))
+    # the library's RCCL gather (ncclGather over one communicator per device) on
+    # distinct devices; peer copies, explicitly, when a rehearsal repeats a device
+    import copy
+    p = copy.copy(p)
+    p.gather = tipe_rt.types.RT_GATHER_RCCL if len(set(devs)) == len(devs) else tipe_rt.types.RT_GATHER_PEER
     dev = torch.device("cuda", devs[0])
     st = torch.cuda.current_stream(dev)
     try:
@@ -546,12 +554,14 @@ def single_process_leg(scene, p, world, devs, steps, verify_ref=None):
             tipe_rt.render_gather_async(scene, p, TILE_ROWS, full.data_ptr(), stream=st.cuda_stream)
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
+        transport = tipe_rt.last_gather_transport()
     finally:
         L.rt_shutdown()
         tipe_rt.check(L.rt_init(0, None))
     rec = {"value": round(W * H * SPP * steps / dt / 1e6, 3), "unit": "Msamples/s", "devices": list(devs),
            "distinct_devices": len(set(devs)), "steps": steps, "ms_per_step": round(dt / steps * 1e3, 3),
-           "entry_point": "rt_render_gather_async (include/rt/rt.h)", "payload": "canva plane, float64"}
+           "entry_point": "rt_render_gather_async (include/rt/rt.h)", "payload": "canva plane, float64",
+           "transport": transport}
     if ok is not None:
         rec["verified_vs_single_device"] = ok
     return rec

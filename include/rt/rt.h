@@ -32,8 +32,14 @@ extern "C" {
  *    rt_params_init so new fields read their defaults.  rt_gather_async.
  * 3: RT_CNT_BVH_STACK_OVER appended (RT_NCOUNTERS 17 -> 18): d_counters
  *    arrays of rt_count_async hold RT_NCOUNTERS entries; scenes above 65534
- *    spheres upload (exact sphere scans) instead of RT_EUNSUPPORTED.      */
-#define RT_ABI_VERSION 3
+ *    spheres upload (exact sphere scans) instead of RT_EUNSUPPORTED.
+ * 4: rt_params gained `gather` (RT_GATHER_*: rt_render_gather_async moves
+ *    the slots' planes with an RCCL ncclGather by default, peer copies only
+ *    on request); rt_abi_version(), rt_last_gather_transport();
+ *    rt_set_fill_precision(RT_PREC_FP32) returns RT_EUNSUPPORTED.
+ * A caller compares rt_abi_version() with the RT_ABI_VERSION it was built
+ * against before passing rt_params or counter arrays.                   */
+#define RT_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------- */
 #define RT_OK            0
@@ -94,7 +100,20 @@ typedef struct rt_params {
     int sky_mode;                      /* RT_SKY_*                                */
     int semantics;                     /* RT_SEM_*: whose integrator               */
     int precision;                     /* RT_PREC_*: arithmetic of the integrator  */
+    int gather;                        /* RT_GATHER_*: multi-device frame transport
+                                          (rt_render_gather_async)            */
 } rt_params;
+
+/* rt_params.gather: how rt_render_gather_async brings the device slots'
+ * planes to the first device.  RCCL (default): one RCCL communicator per
+ * device of rt_init's list (ncclCommInitAll, made once per list) and one
+ * ncclGather of each slot's planes to rank 0 over xGMI, then the assemble
+ * kernel; the devices must be distinct (a list naming a device twice is
+ * RT_EUNSUPPORTED -- RCCL has one rank per GPU).  PEER: hipMemcpyPeerAsync
+ * per slot (also for a list that repeats a device).  Neither falls back to
+ * the other; rt_last_gather_transport() names the one a call used. */
+#define RT_GATHER_RCCL 0
+#define RT_GATHER_PEER 1
 
 /* rt_params.semantics.  MAIN_C (default) is main.c, the authoritative CPU
  * path.  CUDA is main_cuda.cu's integrator, the reference's
@@ -187,7 +206,7 @@ static inline long long rt_chunk_bound(long long c, long long S, long long P)
 
 /* Fills defaults: RT_RNG_PHILOX, seed 1010 (main_cuda.cu's curand seed),
  * compat_int_truncation 1, spp_chunks RT_SPP_CHUNKS_AUTO, RT_ACCEL_AUTO,
- * everything else zero. */
+ * RT_GATHER_RCCL, everything else zero. */
 void rt_params_init(rt_params* p);
 
 /* ---- lifecycle ---------------------------------------------------------- */
@@ -197,13 +216,15 @@ void rt_params_init(rt_params* p);
 int  rt_init(int ndev, const int* devices);
 void rt_shutdown(void);
 const char* rt_last_error(void);
+/* RT_ABI_VERSION of the loaded library. */
+int rt_abi_version(void);
 /* Name of the render kernel the calling thread's last render launch used
  * ("render_kernel_q<QB=0|3|4>" = the task-queue kernel without a BVH / with
  * a deep / shallow tree; "render_kernel_q<QB=-1>" / "<QB=-2>" = its
  * sphere-only instantiations (-2: every material opaque); "<QB=3,OP>" = the
  * deep-tree one for scenes whose every material is opaque;
  * "render_kernel<BVH>" / "render_kernel" = the fixed-grid kernels,
- * "render_kernel_cuda", "render_kernel_f32"); "none" before the first.
+ * "render_kernel_cuda"); "none" before the first.
  * The choice never changes a result.  Diagnostics and tests. */
 const char* rt_last_render_kernel(void);
 const char* rt_version(void);
@@ -234,8 +255,10 @@ void* rt_fill_canva(void* thread_data);
 int rt_set_fill_spp_chunks(int spp_chunks);
 
 /* The rt_params.precision rt_fill_canva renders with.  Since r05 always
- * RT_PREC_FP64 (RT_PREC_FP32 was removed, see rt_params.precision): any
- * argument selects FP64.  Process-wide; returns the previous setting. */
+ * RT_PREC_FP64 (RT_PREC_FP32 was removed, see rt_params.precision):
+ * RT_PREC_FP64 returns the previous setting, anything else is refused
+ * (RT_PREC_FP32: RT_EUNSUPPORTED, other values: RT_EINVAL) and changes
+ * nothing.  Process-wide. */
 int rt_set_fill_precision(int precision);
 
 /* rt_render_rows / rt_fill_canva keep the uploaded scene (and its BVH) of
@@ -303,6 +326,10 @@ int rt_gather_async(int world, const int* src_devices, const rt_color* const* lo
                     int rows_per_rank, int W, int H, int dst_device, rt_color* out, void* hip_stream);
 int rt_render_gather_async(const rt_scene* scene, const rt_params* params, int tile_rows, const rt_frame* frame,
                            void* hip_stream);
+/* The transport the calling thread's last rt_render_gather_async used:
+ * "rccl: ncclGather, RCCL x.y.z (library path), N ranks" or "peer:
+ * hipMemcpyPeerAsync, N slots"; "none" before the first. */
+const char* rt_last_gather_transport(void);
 /* Peer access the gathers use from dst_device to src_device, enabled on
  * first use per pair: 1 = enabled (copy engines read over xGMI; also the
  * answer for dst == src), 0 = unavailable or refused by the runtime (e.g.
@@ -340,12 +367,16 @@ enum {
     RT_CNT_SHADE_LANE_SLOTS, /* 64 x wave-level hit resolutions (bounce
                              shading or AO tail; GPU diagnostic)         */
     RT_CNT_BVH_STACK_OVER, /* BVH stack pushes made at a depth >= the LDS
-                             stack of the kernel that renders this tree
-                             (the queue kernel's 24 / 14 entries, else the
-                             fixed grid's 48).  Must be 0: the host admits a
+                             stack of the kernel a render of the same params
+                             takes (the queue kernel's 24 / 32 / 14 entries,
+                             else the fixed grid's 48; rt_kernels.hip
+                             choose_render).  Must be 0: the host admits a
                              tree by its exact stack bound (rt_bvh.cpp); a
                              nonzero count means that bound is wrong (GPU
-                             diagnostic, rt_count_async only)            */
+                             diagnostic, rt_count_async only).  The
+                             counting walk drops pushes beyond 48 entries,
+                             so when this is nonzero the BVH node and
+                             triangle counts may be too low            */
     RT_NCOUNTERS
 };
 /* Same traversal as rt_render_async, no frame; adds event counts into the

@@ -47,6 +47,8 @@ def test_library_loads_and_reports_version():
     p = T.Params()
     L.rt_params_init(C.byref(p))
     assert p.rng == T.RT_RNG_PHILOX and p.seed == 1010 and p.compat_int_truncation == 1 and p.spp_chunks == T.RT_SPP_CHUNKS_AUTO
+    assert p.gather == T.RT_GATHER_RCCL
+    assert L.rt_abi_version() == T.RT_ABI_VERSION
 
 
 LAYOUT_C = r"""
@@ -61,7 +63,8 @@ int main(void) {
   O(rt_material, alpha); O(rt_triangle, uvB); O(rt_thread_data, nbRayonParPixel);
   O(rt_thread_data, triangle_list); O(rt_thread_data, AO_intensity); O(rt_scene, quelMatPourTri);
   O(rt_params, cam); O(rt_params, focus_distance); O(rt_params, rng); O(rt_params, spp_chunks);
-  O(rt_params, seed); O(rt_params, semantics); O(rt_params, precision); O(rt_frame, radiance);
+  O(rt_params, seed); O(rt_params, semantics); O(rt_params, precision); O(rt_params, gather);
+  O(rt_frame, radiance);
   return 0;
 }
 """

@@ -2,11 +2,14 @@
 
 rt_render_gather_async renders the cyclic row tiles of a frame on every
 device slot of rt_init's list, gathers the slots' planes onto the first
-device with peer copies (xGMI between distinct GPUs) and un-permutes them
-with the assemble kernel -- the device-destination replacement of
-main_cuda.cu:280-339.  The one-GPU box runs several slots on GPU 0 (the
-peer copy is then a device-local copy); the images must equal the oracle's
-bit for bit, since the Philox stream is keyed by the global pixel.
+device and un-permutes them with the assemble kernel -- the
+device-destination replacement of main.c:404-453 / main_cuda.cu:280-339.
+The gather is an RCCL ncclGather over one communicator per device
+(rt_params.gather = RT_GATHER_RCCL, the default) or, on request, peer copies
+(RT_GATHER_PEER).  RCCL has one rank per GPU, so the one-GPU box runs the
+RCCL path as a 1-rank communicator and several slots on GPU 0 through the
+peer path (the copy is then device-local); the images must equal the
+oracle's bit for bit, since the Philox stream is keyed by the global pixel.
 """
 import ctypes as C
 import os
@@ -22,6 +25,10 @@ import tipe_rt
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+PEER = tipe_rt.types.RT_GATHER_PEER
+RCCL = tipe_rt.types.RT_GATHER_RCCL
 
 
 def _slots(n):
@@ -47,6 +54,7 @@ def test_render_gather_slots_bitexact(slots, tile_rows, chunks, scene):
         else:
             bundle = helpers.pyramid_scene()
             p = helpers.params(W, H, 8, 6, chunks=chunks)
+        p.gather = PEER                    # slots on one GPU: peer copies (RCCL has one rank per GPU)
         ref = helpers.oracle_render(bundle, p)
         planes = torch.full((4, H, W, 3), -2.0, dtype=torch.float64, device="cuda:0")
         st = torch.cuda.current_stream().cuda_stream
@@ -55,6 +63,7 @@ def test_render_gather_slots_bitexact(slots, tile_rows, chunks, scene):
         got = planes.cpu().numpy()
         for k, name in enumerate(("canva", "albedo", "normal", "radiance")):
             assert (got[k] == ref[name]).all(), name
+        assert tipe_rt.last_gather_transport().startswith("peer:")
     finally:
         lib.rt_shutdown()
         tipe_rt.check(lib.rt_init(0, None))
@@ -69,6 +78,7 @@ def test_render_gather_canva_only_and_repeat():
         bundle = helpers.cornell()
         W, H = 64, 48
         p = helpers.params(W, H, 6, 5, chunks=3)
+        p.gather = PEER
         ref = helpers.oracle_render(bundle, p)
         st = torch.cuda.current_stream().cuda_stream
         outs = []
@@ -79,6 +89,63 @@ def test_render_gather_canva_only_and_repeat():
         torch.cuda.synchronize()
         for c in outs:
             assert (c.cpu().numpy() == ref["canva"]).all()
+    finally:
+        lib.rt_shutdown()
+        tipe_rt.check(lib.rt_init(0, None))
+
+
+@pytest.mark.parametrize("scene,planes_wanted", [("pyramid", 4), ("tree", 4), ("cornell", 1)])
+def test_rccl_gather_one_device_bitexact(scene, planes_wanted):
+    """RT_GATHER_RCCL (the default) through the whole path on the one-GPU box:
+    rt_init(1, {0}) -> a 1-rank RCCL communicator (ncclCommInitAll), the
+    slot's planes gathered to rank 0 by ncclGather and assembled; bit for
+    bit vs the oracle, twice (the communicator is reused)."""
+    import torch
+    lib = tipe_rt.lib()
+    tipe_rt.check(lib.rt_init(1, (C.c_int * 1)(0)))
+    try:
+        W, H = 52, 41
+        if scene == "tree":
+            bundle = helpers.tree_scene()
+            p = helpers.params(W, H, 8, 8, use_ao=True, ao=2.5, chunks=4)
+        elif scene == "pyramid":
+            bundle = helpers.pyramid_scene()
+            p = helpers.params(W, H, 8, 6, chunks=32)
+        else:
+            bundle = helpers.cornell()
+            p = helpers.params(W, H, 6, 5, chunks=3)
+        assert p.gather == RCCL
+        ref = helpers.oracle_render(bundle, p)
+        st = torch.cuda.current_stream().cuda_stream
+        for _ in range(2):
+            planes = torch.full((4, H, W, 3), -2.0, dtype=torch.float64, device="cuda:0")
+            ptrs = [planes[k].data_ptr() if k < planes_wanted else None for k in range(4)]
+            tipe_rt.render_gather_async(bundle.scene, p, 1, *ptrs, stream=st)
+            torch.cuda.synchronize()
+            got = planes.cpu().numpy()
+            for k, name in enumerate(("canva", "albedo", "normal", "radiance")[:planes_wanted]):
+                assert (got[k] == ref[name]).all(), name
+            assert tipe_rt.last_gather_transport().startswith("rccl: ncclGather"), tipe_rt.last_gather_transport()
+    finally:
+        lib.rt_shutdown()
+        tipe_rt.check(lib.rt_init(0, None))
+
+
+def test_rccl_gather_refuses_a_repeated_device():
+    """No silent fallback: RCCL has one rank per GPU, so a device list that
+    names a GPU twice is RT_EUNSUPPORTED under RT_GATHER_RCCL."""
+    import torch
+    lib = _slots(2)
+    try:
+        bundle = helpers.cornell()
+        p = helpers.params(16, 12, 2, 4)
+        c = torch.zeros((12, 16, 3), dtype=torch.float64, device="cuda:0")
+        fr = tipe_rt.Frame(c.data_ptr(), None, None, None)
+        assert lib.rt_render_gather_async(C.byref(bundle.scene), C.byref(p), 1, C.byref(fr), None) == \
+            tipe_rt.RT_EUNSUPPORTED
+        assert b"RT_GATHER_PEER" in lib.rt_last_error()
+        p.gather = 7
+        assert lib.rt_render_gather_async(C.byref(bundle.scene), C.byref(p), 1, C.byref(fr), None) == tipe_rt.RT_EINVAL
     finally:
         lib.rt_shutdown()
         tipe_rt.check(lib.rt_init(0, None))
@@ -164,10 +231,11 @@ def _device_count():
         return 0
 
 
-@pytest.mark.parametrize("peer_env", ["1", "0"])
-def test_render_gather_distinct_devices_bitexact(peer_env):
-    """Slots on distinct GPUs: peer enable (or, with RT_PEER_ACCESS=0, the
-    runtime's staged copies), cross-device event waits and xGMI copies.
+@pytest.mark.parametrize("peer_env,gather", [("1", 1), ("0", 1), ("1", 0)])
+def test_render_gather_distinct_devices_bitexact(peer_env, gather):
+    """Slots on distinct GPUs: RCCL (gather 0: a 2-rank communicator and
+    ncclGather over xGMI) or peer copies (gather 1: peer enable or, with
+    RT_PEER_ACCESS=0, the runtime's staged copies), cross-device event waits.
     Needs >= 2 GPUs, so it is skipped on the builder's one-GPU box; run in a
     subprocess so the environment switch applies from the library's first
     peer call."""
@@ -182,6 +250,7 @@ tipe_rt.check(lib.rt_init(2, (C.c_int * 2)(0, 1)))
 bundle = helpers.pyramid_scene()
 W, H = 52, 41
 p = helpers.params(W, H, 8, 6, chunks=4)
+p.gather = %d
 ref = helpers.oracle_render(bundle, p)
 planes = torch.full((4, H, W, 3), -2.0, dtype=torch.float64, device="cuda:0")
 tipe_rt.render_gather_async(bundle.scene, p, 1, *[planes[k].data_ptr() for k in range(4)],
@@ -190,12 +259,15 @@ torch.cuda.synchronize()
 got = planes.cpu().numpy()
 ok = all((got[k] == ref[n]).all() for k, n in enumerate(("canva", "albedo", "normal", "radiance")))
 st = lib.rt_peer_access(0, 1)
+print("TRANSPORT", tipe_rt.last_gather_transport())
 print("RESULT", int(ok), st)
-''' % ([os.path.join(ROOT, "tests"), os.path.join(ROOT, "tipe-raytracer_amd")],)
+''' % ([os.path.join(ROOT, "tests"), os.path.join(ROOT, "tipe-raytracer_amd")], gather)
     env = dict(os.environ, RT_PEER_ACCESS=peer_env)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     res = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][-1].split()
     assert res[1] == "1"
-    if peer_env == "0":
+    tr = [ln for ln in r.stdout.splitlines() if ln.startswith("TRANSPORT")][-1]
+    assert ("rccl: ncclGather" if gather == 0 else "peer:") in tr
+    if peer_env == "0" and gather == 1:
         assert res[2] == "0"

@@ -37,7 +37,10 @@ def test_oracle_refuses_fp32():
                                                   None, None, None, None) == T.RT_EINVAL
 
 
-def test_fill_precision_setter_always_fp64():
+def test_fill_precision_setter_refuses_fp32():
+    """asking the drop-in for FP32 is an error, not a silent FP64."""
     L = tipe_rt.lib()
-    L.rt_set_fill_precision(T.RT_PREC_FP32)
+    assert L.rt_set_fill_precision(T.RT_PREC_FP32) == T.RT_EUNSUPPORTED
+    assert b"removed" in L.rt_last_error()
+    assert L.rt_set_fill_precision(9) == T.RT_EINVAL
     assert L.rt_set_fill_precision(T.RT_PREC_FP64) == T.RT_PREC_FP64

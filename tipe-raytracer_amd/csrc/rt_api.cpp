@@ -21,6 +21,7 @@
 #include "rt/rt.h"
 #include "rt_internal.h"
 #include "rt_bvh.h"
+#include "rt_rccl.h"
 
 using namespace rt;
 
@@ -109,6 +110,8 @@ int validate_params(const rt_params* p)
         return fail(RT_EUNSUPPORTED, "RT_PREC_FP32 was removed (r05): its 1.1-3.4e-4 per-channel RMSE against the "
                                      "reference exceeded north_star's 1e-4; only the bit-exact FP64 path renders");
     if (p->precision != RT_PREC_FP64) return fail(RT_EINVAL, "unknown precision %d", p->precision);
+    if (p->gather != RT_GATHER_RCCL && p->gather != RT_GATHER_PEER)
+        return fail(RT_EINVAL, "unknown gather transport %d", p->gather);
     if ((unsigned long long)p->largeur_image * (unsigned long long)p->hauteur_image > 0xffffffffull)
         return fail(RT_EUNSUPPORTED, "pixel index exceeds the 32-bit Philox counter word");
     return RT_OK;
@@ -720,9 +723,11 @@ void rt_shutdown(void)
     }
     scene_cache_clear();
     stream_pool_clear();
+    rccl_release();
 }
 
 const char* rt_last_error(void) { return g_err.c_str(); }
+int rt_abi_version(void) { return RT_ABI_VERSION; }
 const char* rt_last_render_kernel(void) { return last_render_kernel(); }
 
 const char* rt_version(void)
@@ -1172,6 +1177,12 @@ int rt_gather_async(int world, const int* src_devices, const rt_color* const* lo
     return rc;
 }
 
+namespace {
+thread_local std::string g_gather_transport = "none";
+}
+
+const char* rt_last_gather_transport(void) { return g_gather_transport.c_str(); }
+
 int rt_render_gather_async(const rt_scene* scene, const rt_params* params, int tile_rows, const rt_frame* frame,
                            void* hip_stream)
 {
@@ -1186,6 +1197,18 @@ int rt_render_gather_async(const rt_scene* scene, const rt_params* params, int t
         devs = g_devices;
     }
     const int G = (int)devs.size(), W = params->largeur_image, H = params->hauteur_image;
+    // RT_GATHER_RCCL: one rank per device, so the list must not repeat one; the
+    // communicators are made (once per list) before anything is enqueued
+    const bool rccl = params->gather == RT_GATHER_RCCL;
+    if (rccl) {
+        for (int a = 0; a < G; ++a)
+            for (int b = a + 1; b < G; ++b)
+                if (devs[(size_t)a] == devs[(size_t)b])
+                    return fail(RT_EUNSUPPORTED, "RT_GATHER_RCCL needs distinct devices (rt_init's list names device %d "
+                                                 "twice; RCCL has one rank per GPU): use RT_GATHER_PEER", devs[(size_t)a]);
+        std::string err;
+        if (rccl_comms(devs, err)) return fail(RT_EDEVICE, "RCCL: %s", err.c_str());
+    }
     const int dst = devs[0];
     const int n_tiles = (((H + tile_rows - 1) / tile_rows) + G - 1) / G;      // per slot (rows >= H skipped)
     const int rows_pr = n_tiles * tile_rows;
@@ -1254,17 +1277,44 @@ int rt_render_gather_async(const rt_scene* scene, const rt_params* params, int t
             if (e != hipSuccess) rc = fail(RT_EDEVICE, "wait: %s", hipGetErrorString(e));
         }
         rt_color* staging = nullptr;
+        const size_t per_slot = rccl ? plane * nplanes : plane;             // colours staged per slot
         if (rc == RT_OK) {
-            const hipError_t e = hipMallocAsync((void**)&staging, (size_t)G * plane * sizeof(rt_color), dst_st);
+            const hipError_t e = hipMallocAsync((void**)&staging, (size_t)G * per_slot * sizeof(rt_color), dst_st);
             if (e != hipSuccess) rc = fail(RT_ENOMEM, "gather staging: %s", hipGetErrorString(e));
         }
-        int k = 0;
-        for (int pl = 0; pl < 4 && rc == RT_OK; ++pl) {
-            if (!outs[pl]) continue;
-            std::vector<const rt_color*> loc((size_t)G);
-            for (int q = 0; q < G; ++q) loc[(size_t)q] = slots[(size_t)q].buf + (size_t)k * plane;
-            rc = gather_plane(G, devs.data(), loc.data(), tile_rows, rows_pr, W, H, dst, staging, outs[pl], dst_st);
-            ++k;
+        if (rccl && rc == RT_OK) {
+            // every slot's planes (contiguous in its buffer) in one ncclGather to
+            // rank 0, rank 0's part on hip_stream (which waited for its render),
+            // the others' on their own streams after their renders; then one
+            // assemble per plane from the rank-major staging
+            std::vector<const void*> send((size_t)G);
+            std::vector<hipStream_t> sst((size_t)G);
+            for (int q = 0; q < G; ++q) {
+                send[(size_t)q] = slots[(size_t)q].buf;
+                sst[(size_t)q] = q == 0 ? dst_st : slots[(size_t)q].ps->st;
+            }
+            std::string err;
+            if (rccl_gather(devs, send, staging, per_slot * 3, sst, err)) rc = fail(RT_EDEVICE, "RCCL: %s", err.c_str());
+            for (int k = 0; k < nplanes && rc == RT_OK; ++k) {
+                int pl = -1;
+                for (int j = 0, m = 0; j < 4; ++j)
+                    if (outs[j] && m++ == k) pl = j;
+                const int e = launch_assemble((const double*)(staging + (size_t)k * plane), (long long)per_slot, G,
+                                              tile_rows, rows_pr, W, H, (double*)outs[pl], dst_st);
+                if (e) rc = fail(RT_EDEVICE, "assemble launch: %s", hipGetErrorString((hipError_t)e));
+            }
+            if (rc == RT_OK)
+                g_gather_transport = "rccl: ncclGather, " + rccl_describe() + ", " + std::to_string(G) + " ranks";
+        } else {
+            int k = 0;
+            for (int pl = 0; pl < 4 && rc == RT_OK; ++pl) {
+                if (!outs[pl]) continue;
+                std::vector<const rt_color*> loc((size_t)G);
+                for (int q = 0; q < G; ++q) loc[(size_t)q] = slots[(size_t)q].buf + (size_t)k * plane;
+                rc = gather_plane(G, devs.data(), loc.data(), tile_rows, rows_pr, W, H, dst, staging, outs[pl], dst_st);
+                ++k;
+            }
+            if (rc == RT_OK) g_gather_transport = "peer: hipMemcpyPeerAsync, " + std::to_string(G) + " slots";
         }
         if (staging) (void)hipFreeAsync(staging, dst_st);
         if (rc == RT_OK) {
@@ -1465,7 +1515,10 @@ int rt_set_fill_spp_chunks(int spp_chunks)
 }
 int rt_set_fill_precision(int precision)
 {
-    (void)precision;                 // RT_PREC_FP32 was removed (r05): rt_fill_canva renders FP64
+    // RT_PREC_FP32 was removed (r05): rt_fill_canva renders FP64 only
+    if (precision == RT_PREC_FP32)
+        return fail(RT_EUNSUPPORTED, "RT_PREC_FP32 was removed (r05); rt_fill_canva renders FP64");
+    if (precision != RT_PREC_FP64) return fail(RT_EINVAL, "unknown precision %d", precision);
     return g_fill_prec.exchange(RT_PREC_FP64);
 }
 int rt_scene_cache_clear(void) { return scene_cache_clear(); }

@@ -50,6 +50,8 @@ def lib():
         L.rt_last_error.restype = C.c_char_p
         L.rt_version.restype = C.c_char_p
         L.rt_last_render_kernel.restype = C.c_char_p
+        L.rt_last_gather_transport.restype = C.c_char_p
+        L.rt_abi_version.restype = C.c_int
         L.rt_render_rows.argtypes = [P(Scene), P(Params), C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         L.rt_fill_canva.argtypes = [C.c_void_p]
         L.rt_fill_canva.restype = C.c_void_p
@@ -150,6 +152,11 @@ def denoise_unpack(color3):
     return out
 
 
+def last_gather_transport():
+    """rt_last_gather_transport(): the transport the thread's last rt_render_gather_async used."""
+    return lib().rt_last_gather_transport().decode()
+
+
 def last_render_kernel():
     """rt_last_render_kernel: the render kernel this thread's last launch used."""
     return lib().rt_last_render_kernel().decode()
@@ -205,7 +212,7 @@ def make_scene(spheres=None, triangles=None, quel_mat=None, mat_list=None, tex_w
 
 def make_params(W, H, spp, bounces, cam, focus=3.0, aperture=(0.0, 0.0), use_ao=False, ao=2.5,
                 seed=1010, rng=RT_RNG_PHILOX, compat=1, chunks=1, accel=0, sky_mode=0, semantics=0,
-                precision=0):
+                precision=0, gather=0):
     p = Params()
     p.largeur_image, p.hauteur_image = W, H
     p.nbRayonParPixel, p.nbRebondMax = spp, bounces
@@ -220,6 +227,7 @@ def make_params(W, H, spp, bounces, cam, focus=3.0, aperture=(0.0, 0.0), use_ao=
     p.sky_mode = sky_mode
     p.semantics = semantics
     p.precision = precision
+    p.gather = gather
     return p
 
 

@@ -48,6 +48,8 @@ RT_ACCEL_AUTO, RT_ACCEL_NONE = 0, 1
 RT_SKY_OFF, RT_SKY_LAST_SPHERE = 0, 1
 RT_SEM_MAIN_C, RT_SEM_CUDA = 0, 1
 RT_PREC_FP64, RT_PREC_FP32 = 0, 1
+RT_GATHER_RCCL, RT_GATHER_PEER = 0, 1
+RT_ABI_VERSION = 4
 
 
 class Vec3(C.Structure):
@@ -129,7 +131,8 @@ class Params(C.Structure):
                 ("AO_intensity", C.c_double), ("useAO", C.c_int),
                 ("compat_int_truncation", C.c_int), ("rng", C.c_int),
                 ("spp_chunks", C.c_int), ("seed", C.c_ulonglong), ("accel", C.c_int),
-                ("sky_mode", C.c_int), ("semantics", C.c_int), ("precision", C.c_int)]
+                ("sky_mode", C.c_int), ("semantics", C.c_int), ("precision", C.c_int),
+                ("gather", C.c_int)]
 
 
 class Tiling(C.Structure):
