@@ -401,6 +401,9 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     double cam = 0.0;
     for (int i = 0; i < 3; ++i) cam = std::max(cam, std::fabs(p->cam.origin.e[i]));
     cam += 0.5 * (std::fabs(ox) + std::fabs(oy));
+    if (!std::isfinite(cam) || !std::isfinite(p->cam.origin.e[0]) || !std::isfinite(p->cam.origin.e[1]) ||
+        !std::isfinite(p->cam.origin.e[2]))
+        cam = HUGE_VAL;                  // std::max drops NaN: no gate below may pass on a NaN camera
     // Zero-throughput exit (rt_kernels.hip LanePath::zero_rc): exact when the
     // shading values are bounded and, with AO, the AO factor stays finite.
     kp.zero_exit = g_zero_exit.load() && p->semantics != RT_SEM_CUDA && sc->mats_bounded &&
@@ -913,6 +916,16 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         const rt_triangle& t = scene->triangle_list[i];
         for (int a = 0; a < 3; ++a)
             coord_max = std::fmax(coord_max, std::fmax(std::fabs(t.A.e[a]), std::fmax(std::fabs(t.B.e[a]), std::fabs(t.C.e[a]))));
+    }
+    // fmax drops NaN operands: a non-finite coordinate anywhere makes the bound
+    // infinite, so the gates that read it (zero_exit, tex_const) hold by construction
+    for (int i = 0; i < scene->nbSpheres; ++i)
+        for (int a = 0; a < 3; ++a)
+            if (!std::isfinite(scene->sphere_list[i].center.e[a])) coord_max = HUGE_VAL;
+    for (int i = 0; i < scene->nbTriangles; ++i) {
+        const rt_triangle& t = scene->triangle_list[i];
+        for (int a = 0; a < 3; ++a)
+            if (!std::isfinite(t.A.e[a]) || !std::isfinite(t.B.e[a]) || !std::isfinite(t.C.e[a])) coord_max = HUGE_VAL;
     }
 
     rt_device_scene* ds = new rt_device_scene();
