@@ -273,8 +273,9 @@ PHILOX_CASES = [
                compat=0, chunks=8, cam=scenes.NATURE_CAMERA, kernel="render_kernel_q<QB=3>",
                what="nature + AO 2.5, 20 bounces"),
     PhiloxCase("main_regime_b20", helpers.main_regime_scene, W=64, H=40, spp=8, bounces=20, chunks=4,
-               cam=scenes.MAIN_CAMERA, kernel="render_kernel_q<QB=4>",
-               what="main()'s camera / mesh scale / radius-1e5 sky, 20 bounces (34 triangles: shallow BVH)"),
+               cam=scenes.MAIN_CAMERA, kernel="render_kernel<BVH>",
+               what="main()'s camera / mesh scale / radius-1e5 sky, 20 bounces (34 triangles of up to ~4000 "
+                    "units: no binary16 nodes, sky hit points beyond R_b, so the fixed-grid BVH kernel)"),
     PhiloxCase("main_regime_ao_b20", helpers.main_regime_scene, W=48, H=30, spp=8, bounces=20, use_ao=True,
                ao=2.5, compat=0, chunks=3, cam=scenes.MAIN_CAMERA, what="main()'s regime + AO 2.5, 20 bounces"),
     PhiloxCase("main_regime_fixed", helpers.main_regime_scene, W=48, H=30, spp=4, bounces=20, chunks=1,

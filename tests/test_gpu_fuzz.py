@@ -130,9 +130,15 @@ def test_random_far_scene_bitexact(seed):
     moved by up to 1000 units, inside a radius-1e5 emissive sky sphere
     (main.c:300-301, 346), so the candidate pass's interval bound
     (Hs = (|o| + L) sqrt(a)) and the BVH padding run at |o|, L ~ 1e3-1e5;
-    0-24 bounces; spp_chunks 1-3; bit for bit vs the oracle."""
+    0-24 bounces; spp_chunks 1-3; bit for bit vs the oracle.  Odd seeds run
+    with the zero-throughput exit off, so paths go on after a sky hit and
+    BVH walks start at |o| ~ 1e5 (per-ray margins, rt_kernels.hip ray32)."""
     bundle, p = random_scene(seed, far=True)
-    check_parity(bundle, p)
+    if seed % 2:
+        with tipe_rt.reference_counts():
+            check_parity(bundle, p)
+    else:
+        check_parity(bundle, p)
 
 
 @pytest.mark.parametrize("seed", range(200, 248))

@@ -123,26 +123,37 @@ def test_bvh_stack_bound_holds_on_the_gpu(scene):
     assert c[tipe_rt.types.RT_CNT_BVH_NODES] > 0          # the tree was walked
 
 
-def _nature(opaque):
+def _nature(opaque, far_z=4e4):
+    """RTX_MAP/nature plus one 0.1-unit triangle at z = far_z, behind the
+    camera: the triangles' coordinate bound R_b becomes 4e4, which widens
+    every box's padding, and the tree's exact stack bound becomes 26."""
+    from tipe_rt.types import Triangle
+    import ctypes as C
     tris, qm, mats, tw, th, nm = scenes.nature_mesh()
+    n = len(tris)
+    t2, q2 = (Triangle * (n + 1))(), (C.c_int * (n + 1))()
+    C.memmove(t2, tris, C.sizeof(Triangle) * n)
+    C.memmove(q2, qm, C.sizeof(C.c_int) * n)
+    for P, xy in ((t2[n].A, (0.0, 0.0)), (t2[n].B, (0.1, 0.0)), (t2[n].C, (0.0, 0.1))):
+        P.e[0], P.e[1], P.e[2] = xy[0], xy[1], far_z
+    q2[n] = 0
     if opaque:                          # every texel at alpha 1, no material index 3 / 4 override
         for k in range(len(mats)):
             mats[k].alpha = 1.0
-        for k in range(len(tris)):
-            if qm[k] in (3, 4):
-                qm[k] = 0
-    return helpers.SceneBundle(scenes.main_spheres(), (tris, qm, mats, tw, th, nm))
+        for k in range(n + 1):
+            if q2[k] in (3, 4):
+                q2[k] = 0
+    return helpers.SceneBundle(scenes.main_spheres(), (t2, q2, mats, tw, th, nm))
 
 
 @pytest.mark.parametrize("opaque", [False, True])
 def test_tree_with_stack_bound_above_24_keeps_the_queue_kernel(opaque):
-    """RTX_MAP/nature under main.c:346's radius-1e5 sky: the scene radius
-    (1e5) widens every triangle's padding (rt_bvh.cpp), and the tree's exact
-    stack bound becomes 25 > 24.  The non-opaque deep-tree kernel has 32 LDS
-    stack entries (kStackQN; 38 KiB per block, still 4 blocks per CU), so it
-    takes such trees -- an opaque one too, instead of the 24-entry OPQ
-    kernel -- rather than the fixed grid; every push stays inside
-    (RT_CNT_BVH_STACK_OVER == 0), bit for bit vs the oracle."""
+    """A tree whose exact stack bound is 26 (> 24, _nature above).  The
+    non-opaque deep-tree kernel has 32 LDS stack entries (kStackQN; 38 KiB
+    per block, still 4 blocks per CU), so it takes such trees -- an opaque
+    one too, instead of the 24-entry OPQ kernel -- rather than the fixed
+    grid; every push stays inside (RT_CNT_BVH_STACK_OVER == 0), bit for bit
+    vs the oracle."""
     from test_gpu_parity import assert_stack_bound_holds
     bundle = _nature(opaque)
     p = helpers.params(32, 24, 4, 10, chunks=4, cam=helpers.camera_of(scenes.NATURE_CAMERA))

@@ -155,7 +155,8 @@ struct rt_device_scene {
     int sky_w = 0, sky_h = 0;
     int* tri_orig = nullptr;         // leaf order -> caller's triangle index
     int bvh_nodes = 0, bvh_depth = 0, bvh_stack4 = 0;
-    double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0;
+    double s_rel = 0.0, s_abs = 0.0, r_scene = 0.0, k_delta = 0.0;
+    double sph_bound = 0.0;          // max over spheres of max_a |c_a| + r (+inf for a non-finite one)
     float bvh_rbox = 0.0f;           // >= every |bound| of the BVH's boxes
     bool mats_bounded = false;       // every diffuse/emission/strength finite, |x| <= 2^100
     bool sph_opaque = false;         // every sphere material takes main.c's opaque branch (no hole, no refraction)
@@ -413,11 +414,24 @@ int make_kparams(const rt_device_scene* sc, const rt_params* p, const rt_tiling*
     // below 2^205 and areaABC >= |N| (1 - 2^-50) with |N| >= 1e-6 / |d| for any
     // hit (det >= 1e-6), so the barycentrics are finite and u = v = +-0
     kp.tex_const = sc->all_tex0 && std::fmax(sc->coord_max, cam) <= 0x1p100;
-    if (sc->bvh && p->accel == RT_ACCEL_AUTO && cam <= sc->r_scene) {
+    // (origins beyond r_scene -- the camera, hit points on far spheres -- widen
+    // the walk's margins per ray, rt_kernels.hip ray32; a non-finite camera
+    // takes the every-triangle scan)
+    if (sc->bvh && p->accel == RT_ACCEL_AUTO && std::isfinite(cam)) {
         kp.bvh = sc->bvh;
         kp.bvhh = sc->bvhh;
         kp.bvh_srel = sc->s_rel;
         kp.bvh_sabs = sc->s_abs;
+        kp.bvh_rb = sc->r_scene;
+        kp.bvh_kdelta = sc->k_delta;
+        {
+            float rf = (float)sc->r_scene;            // rb_f (1 + 2^-23) <= R_b
+            while (rf > 0.0f && (double)rf * (1.0 + 0x1p-23) > sc->r_scene) rf = std::nextafter(rf, 0.0f);
+            kp.bvh_rb_f = rf;
+            // origins: the camera (+ aperture), hit points on the spheres and on
+            // the triangles (inside R_b by construction)
+            kp.bvh_far = !(cam <= sc->r_scene && sc->sph_bound <= sc->r_scene);
+        }
         kp.bvh_rbox = sc->bvh_rbox;
         // the traversal stack's uint16 entries (node indices): entries the tree can
         // need (rt_bvh.cpp's exact bound), or more than any stack when an index
@@ -863,20 +877,30 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
         tri_mat[i] = to_dev(t.mat);
     }
     // Triangle BVH (rt_bvh.cpp) over scenes with more than 32 triangles; the
-    // triangle arrays are then stored in leaf order.  r_scene bounds every
-    // coordinate a ray origin can take on the scene's surfaces.
+    // triangle arrays are then stored in leaf order.  r_scene bounds the
+    // triangles' coordinates (so every hit point on them) and the spheres
+    // whose hit points cost the padding little (bvh_origin_radius); the padding
+    // assumes origins within it, and rays from farther out (the camera, hit
+    // points on large spheres such as main.c:346's radius-1e5 sky) widen the
+    // walk's margins by the rest (rt_kernels.hip ray32).  Against r_scene over
+    // every sphere: RTX_MAP/nature under the sky 700 -> 808 Msamples/s at 64 spp
+    // (r06, tools/probes/nature_radius.py)
     BvhBuild bvh;
     if (scene->nbTriangles > 32) {           // (a BVH over C3's 5 triangles: 5118 -> 4482 Msamples/s)
         double r = 1.0;
-        for (int i = 0; i < scene->nbSpheres; ++i) {
-            const rt_sphere& q = scene->sphere_list[i];
-            for (int a = 0; a < 3; ++a) r = std::max(r, std::fabs(q.center.e[a]) + std::fabs(q.radius));
-        }
         for (int i = 0; i < scene->nbTriangles; ++i) {
             const rt_triangle& t = scene->triangle_list[i];
             for (int a = 0; a < 3; ++a)
                 r = std::max({r, std::fabs(t.A.e[a]), std::fabs(t.B.e[a]), std::fabs(t.C.e[a])});
         }
+        std::vector<double> sb((size_t)scene->nbSpheres);
+        for (int i = 0; i < scene->nbSpheres; ++i) {
+            const rt_sphere& q = scene->sphere_list[i];
+            double b = 0.0;
+            for (int a = 0; a < 3; ++a) b = std::max(b, std::fabs(q.center.e[a]) + std::fabs(q.radius));
+            sb[(size_t)i] = std::isfinite(b) ? b : HUGE_VAL;
+        }
+        if (std::isfinite(r)) r = bvh_origin_radius(tri.data(), scene->nbTriangles, r, sb.data(), scene->nbSpheres);
         if (std::isfinite(r) && build_bvh(tri.data(), scene->nbTriangles, r, bvh)) {
             std::vector<TriGeo> tri2(tri.size());
             std::vector<TriTex> tex2(tex.size());
@@ -965,6 +989,13 @@ int rt_scene_upload(int device, const rt_scene* scene, rt_device_scene** out)
     ds->s_rel = bvh.s_rel;
     ds->s_abs = bvh.s_abs;
     ds->r_scene = bvh.r_scene;
+    for (int i = 0; i < scene->nbSpheres; ++i) {
+        const rt_sphere& q = scene->sphere_list[i];
+        double b = 0.0;
+        for (int a = 0; a < 3; ++a) b = std::max(b, std::fabs(q.center.e[a]) + std::fabs(q.radius));
+        ds->sph_bound = std::isfinite(b) ? std::max(ds->sph_bound, b) : HUGE_VAL;   // (max keeps +inf)
+    }
+    ds->k_delta = bvh.k_delta;
     {
         float rb = 0.0f;             // the single-precision slab margin's coordinate bound
         for (const BvhNode4& nd : bvh.nodes4)

@@ -224,6 +224,40 @@ int collapse(const std::vector<BvhNode>& bin, int b, std::vector<BvhNode4>& out,
 
 }  // namespace
 
+double bvh_pad_slope(const TriGeo* tri, int nt, double* median_e)
+{
+    double maxE = 0.0;
+    std::vector<double> es((size_t)std::max(nt, 0));
+    for (int i = 0; i < nt; ++i) {
+        const TriGeo& g = tri[i];
+        es[(size_t)i] = norm3(g.abx, g.aby, g.abz) + norm3(g.acx, g.acy, g.acz);
+        maxE = std::max(maxE, es[(size_t)i]);
+    }
+    if (median_e) {
+        *median_e = 0.0;
+        if (nt > 0) {
+            std::nth_element(es.begin(), es.begin() + nt / 2, es.end());
+            *median_e = es[(size_t)(nt / 2)];
+        }
+    }
+    return (maxE * maxE * 4.0 * std::ldexp(1e6, -44) + std::ldexp(1.0, -48)) * (1.0 + std::ldexp(1.0, -40));
+}
+
+double bvh_origin_radius(const TriGeo* tri, int nt, double tri_bound, const double* sphere_bounds, int ns)
+{
+    double med = 0.0;
+    const double k = bvh_pad_slope(tri, nt, &med);
+    // the largest origin radius whose padding stays within 2^-12 of the median
+    // triangle's size: spheres inside it (e.g. the README box's radius-500 walls
+    // around the C4 tree) cost the tree nothing and their hit points no per-ray
+    // margin; larger ones (main.c:346's radius-1e5 sky) stay outside
+    const double cap = std::max(tri_bound, std::ldexp(med, -12) / k);
+    double r = tri_bound;
+    for (int i = 0; i < ns; ++i)
+        if (sphere_bounds[i] <= cap) r = std::max(r, sphere_bounds[i]);
+    return r;
+}
+
 bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
 {
     out = BvhBuild();
@@ -315,7 +349,12 @@ bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out)
     out.s_rel = k + std::ldexp(1.0, -48);
     out.s_abs = k * r_scene + std::ldexp(r_scene, -48);
     out.r_scene = r_scene;
-    return true;
+    // delta(R) above is affine in R with slope (e1+e2)^2 4 2^-44 1e6 + 2^-48, the
+    // distance slack S_abs = s_rel R: a ray from |o|_inf = R' > r_scene needs the
+    // boxes wider by at most k_delta (R' - r_scene) and S_abs = s_rel R' (the walk
+    // adds both per ray, rt_kernels.hip ray32); rounded up
+    out.k_delta = bvh_pad_slope(tri, nt, nullptr);
+    return std::isfinite(out.k_delta);
 }
 
 // ---- 64-byte nodes (BvhNodeH) ------------------------------------------------

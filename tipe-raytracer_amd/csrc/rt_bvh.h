@@ -70,11 +70,22 @@ struct BvhBuild {
     int stack4 = 0;                 // traversal stack entries the tree can need (<= 3 * depth4; <= kStack4)
     double s_rel = 0.0, s_abs = 0.0;   // distance-cull slack (rt_bvh.cpp header)
     double r_scene = 0.0;              // coordinate bound the padding assumed
+    double k_delta = 0.0;              // >= d(padding)/dR of every triangle: a ray whose origin
+                                       // lies at R' > r_scene widens the boxes by k_delta (R' - r_scene)
 };
 
-// Builds over nt precomputed triangles whose coordinates (and every ray
-// origin) are bounded by r_scene in magnitude.  false: no BVH (too few
-// triangles or too many nodes) -> brute-force scan.
+// Builds over nt precomputed triangles whose coordinates are bounded by
+// r_scene in magnitude; the padding assumes ray origins within r_scene too,
+// and the walk widens it per ray for origins beyond (k_delta, rt_kernels.hip
+// ray32).  false: no BVH (too few triangles or too many nodes) -> brute-force
+// scan.
 bool build_bvh(const TriGeo* tri, int nt, double r_scene, BvhBuild& out);
+// >= d(padding)/dR of every triangle (BvhBuild::k_delta); median_e: the
+// median e1 + e2 (may be null).
+double bvh_pad_slope(const TriGeo* tri, int nt, double* median_e);
+// The origin radius to build with: the triangles' coordinate bound, raised to
+// cover every sphere (sphere_bounds[i] = max_a |c_a| + r) whose hit points the
+// padding can include at a cost below 2^-12 of the median triangle's size.
+double bvh_origin_radius(const TriGeo* tri, int nt, double tri_bound, const double* sphere_bounds, int ns);
 
 }  // namespace rt

@@ -150,6 +150,10 @@ struct KParams {
                              // spheres, whose slots do not fit RT_CAND_TAG's 16 bits)
     int stack_cap;           // BVH stack entries of the kernel launch_render picks for this launch
                              // (choose_render; host-set): what COUNT runs check pushes against
+    double bvh_rb;           // the origin bound R_b the tree's padding assumed (rt_bvh.h r_scene)
+    double bvh_kdelta;       // padding growth per unit of origin beyond it (rt_bvh.h k_delta)
+    float bvh_rb_f;          // a float with rb_f (1 + 2^-23) <= R_b (the walk's cheap "inside" test)
+    int bvh_far;             // some ray origin may lie beyond R_b: a sphere or the camera does
 };
 
 // The render kernel launch_render takes and its BVH walk's LDS stack entries

@@ -703,6 +703,18 @@ __device__ __forceinline__ NODE* bvh_top_q()
 // within 6 u (rbox + |o|) |inv| + 2 u E < E / 5 (u = 2^-24).  (These are the
 // min and max of the two plane distances: lo <= hi and a < b order them.)
 // The cull thresholds are rounded outward in the same way.
+// Rays whose origin lies beyond the radius R_b the tree's padding assumed
+// (kp.bvh_rb: the triangles' coordinate bound, raised over the spheres that
+// cost the padding little, rt_bvh.cpp bvh_origin_radius) -- the camera, hit
+// points on main.c:346's radius-1e5 sky sphere -- get the rest of the slack
+// per ray: with R' = max(R_b, |o|_inf) every triangle's padding delta(R) grows
+// by at most kdelta (R' - R_b) (delta is affine in R with slope 4 2^-44 1e6
+// (e1+e2)^2 + 2^-48 <= kdelta, host), i.e. the ray's entry (exit) plane
+// distances move down (up) by that over |d| per axis, and the distance slack
+// S_abs = s_rel R grows by s_rel (R' - R_b), which lowers every entry distance
+// and raises every exit distance by as much (the box test max(tmin, -S_abs)
+// <= min(tmax, best (1 + s_rel) + S_abs) then holds for the larger S_abs).
+// Both fold into the offsets a, b once per ray; the per-node test is unchanged.
 struct Ray32 {
     float ix, iy, iz;            // ~1/d
     float ax, ay, az;            // offsets of the entry planes (lower bounds)
@@ -719,12 +731,33 @@ __device__ __forceinline__ void ray32_axis(double oc, double dc, float rbox, flo
     a = -oi - E;
     b = -oi + E;
 }
-__device__ __forceinline__ Ray32 ray32(const V3 o, const V3 d, float rbox)
+// FAR: compiled into the kernels that may meet such origins (the non-opaque
+// deep-tree queue kernel and the fixed-grid ones); launch_render gives the
+// others (C4's OPQ kernel, QB 4) only launches with kp.bvh_far 0.
+template <bool FAR = true>
+__device__ __forceinline__ Ray32 ray32(const KParams& kp, const V3 o, const V3 d)
 {
     Ray32 r;
-    ray32_axis(o.x, d.x, rbox, r.ix, r.ax, r.bx);
-    ray32_axis(o.y, d.y, rbox, r.iy, r.ay, r.by);
-    ray32_axis(o.z, d.z, rbox, r.iz, r.az, r.bz);
+    ray32_axis(o.x, d.x, kp.bvh_rbox, r.ix, r.ax, r.bx);
+    ray32_axis(o.y, d.y, kp.bvh_rbox, r.iy, r.ay, r.by);
+    ray32_axis(o.z, d.z, kp.bvh_rbox, r.iz, r.az, r.bz);
+    // |(float)o| <= rb_f (host: rb_f (1 + 2^-23) <= R_b) puts o inside R_b;
+    // the others take the exact excess (NaN origins miss every box anyway).
+    // The float roundings of the widened offsets stay inside E's slack.
+    // kp.bvh_far 0 (host: the camera and every sphere lie inside R_b, so every
+    // ray origin does): one scalar branch per ray instead of the test.
+    if (!FAR || !kp.bvh_far) return r;
+    const float omf = fmaxf(fabsf((float)o.x), fmaxf(fabsf((float)o.y), fabsf((float)o.z)));
+    if (!(omf <= kp.bvh_rb_f)) {
+        const double ex = fmax(fmax(fabs(o.x), fmax(fabs(o.y), fabs(o.z))) - kp.bvh_rb, 0.0);
+        const float dpad = (float)(kp.bvh_kdelta * ex) * (1.0f + 0x1p-20f);
+        const float sx = (float)(kp.bvh_srel * ex) * (1.0f + 0x1p-20f);
+        const float px = fmaf(dpad, fabsf(r.ix), sx), py = fmaf(dpad, fabsf(r.iy), sx),
+                    pz = fmaf(dpad, fabsf(r.iz), sx);
+        r.ax -= px; r.bx += px;
+        r.ay -= py; r.by += py;
+        r.az -= pz; r.bz += pz;
+    }
     return r;
 }
 // float(best * srel + sabs) rounded up (the triangle test's distance cull)
@@ -916,7 +949,7 @@ __device__ __forceinline__ void tris_bvh(const KParams& kp, const V3 o, const V3
                                          int& win, int& win_orig, Cnt& cnt)
 {
     unsigned short* stk = bvh_stack();
-    const Ray32 r32 = ray32(o, d, kp.bvh_rbox);
+    const Ray32 r32 = ray32(kp, o, d);
     int node = 0, sp = 0;
     while (bvh_step<COUNT, CU>(kp, o, d, r32, stk, node, sp, best, kind, win, win_orig, cnt)) {
     }
@@ -1618,7 +1651,7 @@ struct LanePath {
         win = cast_spheres<COUNT, false>(kp, o, cd, best, cnt);
         kind = win >= 0 ? HIT_SPHERE : HIT_NONE;
         win_orig = 0;
-        if (kp.bvh) r32 = ray32(o, cd, kp.bvh_rbox);
+        if (kp.bvh) r32 = ray32(kp, o, cd);
         node = 0;
         sp = 0;
         state = SM_TRAV;
@@ -1851,7 +1884,7 @@ __device__ __forceinline__ void samples_coop(const KParams& kp, int x, int g, ui
                 if (fresh) {
                     to = ro;
                     td = rd;
-                    tr32 = ray32(ro, rd, kp.bvh_rbox);
+                    tr32 = ray32(kp, ro, rd);
                 }
             }
             double best = shfl_d(L.best, tr);
@@ -2501,7 +2534,7 @@ void render_kernel_q(const KParams kp)
                 __builtin_amdgcn_s_setprio(RT_WALK_PRIO);
 #endif
                 const V3 dd = L.cast_dir();
-                const Ray32 r32 = ray32(L.o, dd, kp.bvh_rbox);
+                const Ray32 r32 = ray32<QB == 3 && !OPQ>(kp, L.o, dd);
                 unsigned short* stk = bvh_stack_q<QB, OPQ>();
                 const QNode* top = NTOP > 0 ? bvh_top_q<QNode, NTOP>() : nullptr;
 #pragma unroll 1
@@ -3045,8 +3078,8 @@ const char* last_render_kernel() { return t_last_kernel; }
 // 3 for deep ones (kp.bvh_steps, host; compile-time per instantiation).  The
 // deep-tree instantiation walks the 64-byte nodes kp.bvhh: a deep tree that
 // pack_bvh_h refused (a coordinate beyond binary16's range, a leaf index above
-// 65535, an oversized leaf) renders with the fixed-grid kernel; a shallow one
-// keeps the queue kernel.
+// 65535, an oversized leaf) renders with QB 4's walk when its stack fits there,
+// else with the fixed-grid kernel; a shallow one keeps the queue kernel.
 RenderChoice choose_render(const KParams& kp, bool task_ok)
 {
     RenderChoice c;
@@ -3058,12 +3091,17 @@ RenderChoice choose_render(const KParams& kp, bool task_ok)
     bool qbvh = false;
     if (kp.bvh != nullptr && kp.bvh_stack <= kStackQN) {
         c.qb = kp.bvh_steps <= 3 || kp.bvh_stack > kStackQ4 ? 3 : 4;
+        // a deep tree without 64-byte nodes whose stack fits QB 4's walks the
+        // 128-byte nodes there (e.g. main()'s pyramide_eau mesh: triangles of
+        // ~4000 units pad their boxes beyond binary16's range)
+        if (c.qb == 3 && RT_QNODE_H && kp.bvhh == nullptr && kp.bvh_stack <= kStackQ4 && !kp.bvh_far) c.qb = 4;
+        if (c.qb == 4 && kp.bvh_far) c.qb = 3;           // QB 4 has no far-origin margins (ray32<false>)
         qbvh = c.qb == 4 || !RT_QNODE_H || kp.bvhh != nullptr;
     }
     if (task_ok && kp.chunks > 1 && (!kp.bvh || qbvh) && !kp.cuda && !kp.sums) {
         c.queue = true;
         if (!qbvh) c.qb = RT_QSPHERES && kp.nt == 0 ? (RT_QOPAQUE && kp.opaque ? -2 : -1) : 0;
-        c.opq = RT_QOPAQUE_BVH && c.qb == 3 && kp.opaque_all && kp.bvh_stack <= kStackQ;
+        c.opq = RT_QOPAQUE_BVH && c.qb == 3 && kp.opaque_all && kp.bvh_stack <= kStackQ && !kp.bvh_far;
         if (kp.bvh) c.stack_cap = c.qb == 4 ? kStackQ4 : c.opq ? kStackQ : kStackQN;
     }
 #endif
