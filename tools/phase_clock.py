@@ -26,6 +26,8 @@ PHASES = ("sphere_cast", "bvh_walk", "resolve_hit", "task_handout", "next_ray_an
 
 
 def scene_of(kind):
+    if kind == "nature":
+        return tipe_rt.make_scene(scenes.main_spheres(), *scenes.nature_mesh()), 10, False
     sph = scenes.cornell_spheres()
     if kind == "c2":
         return tipe_rt.make_scene(sph), 6, False
@@ -43,7 +45,8 @@ def run(kind, spp):
     if os.path.exists(path):
         os.remove(path)
     sc, bounces, ao = scene_of(kind)
-    cam = tipe_rt.init_camera(**{k: scenes.README_CAMERA[k] for k in ("origin", "target", "up", "vfov", "ratio")})
+    spec = scenes.NATURE_CAMERA if kind == "nature" else scenes.README_CAMERA
+    cam = tipe_rt.init_camera(**{k: spec[k] for k in ("origin", "target", "up", "vfov", "ratio")})
     p = tipe_rt.make_params(1200, 900, spp, bounces, cam, focus=3.0, seed=1010, chunks=32, use_ao=ao, ao=2.5)
     ds = tipe_rt.DeviceScene(sc, 0)
     out = torch.empty((3, 900, 1200, 3), dtype=torch.float64, device="cuda:0")
@@ -70,4 +73,4 @@ if __name__ == "__main__":
     kinds = (sys.argv[1] if len(sys.argv) > 1 else "c2,c3,c4,sweep").split(",")
     spp = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     for k in kinds:
-        print(json.dumps(run(k, spp or (32 if k == "c4" else 128))), flush=True)
+        print(json.dumps(run(k, spp or (32 if k in ("c4", "nature") else 128))), flush=True)
