@@ -680,6 +680,11 @@ __device__ __forceinline__ unsigned short* bvh_stack_q()
 #ifndef RT_QB_TOP
 #define RT_QB_TOP 40
 #endif
+// node visits per round of the non-opaque deep-tree instantiation (the OPQ
+// one and C4: 3, r05_steps)
+#ifndef RT_QN_STEPS
+#define RT_QN_STEPS 3
+#endif
 // the queue kernel walks the 64-byte nodes (BvhNodeH) when the scene has them
 #ifndef RT_QNODE_H
 #define RT_QNODE_H 1
@@ -2538,7 +2543,7 @@ void render_kernel_q(const KParams kp)
                 unsigned short* stk = bvh_stack_q<QB, OPQ>();
                 const QNode* top = NTOP > 0 ? bvh_top_q<QNode, NTOP>() : nullptr;
 #pragma unroll 1
-                for (int j = 0; j < QB; ++j) {
+                for (int j = 0; j < (QB == 3 && !OPQ ? RT_QN_STEPS : QB); ++j) {
                     if (L.state == SM_TRAV) {
                         Cnt cnt;
                         if (!bvh_step<false, false, NTOP, HN>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind, L.win,
