@@ -680,10 +680,18 @@ __device__ __forceinline__ unsigned short* bvh_stack_q()
 #ifndef RT_QB_TOP
 #define RT_QB_TOP 40
 #endif
-// node visits per round of the non-opaque deep-tree instantiation (the OPQ
-// one and C4: 3, r05_steps)
-#ifndef RT_QN_STEPS
-#define RT_QN_STEPS 3
+// node visits per round of the deep-tree instantiations (QB 3): RT_QW_MIN,
+// then more while >= RT_QW_LANES lanes still walk, at most RT_QW_MAX (r06,
+// profiles/r06_walk: RTX_MAP/nature +17 %, C4 / mineways / a non-opaque tree
+// +-0.5 %; a fixed 10 visits gave nature +16 % but the tree -13 %)
+#ifndef RT_QW_MIN
+#define RT_QW_MIN 3
+#endif
+#ifndef RT_QW_MAX
+#define RT_QW_MAX 12
+#endif
+#ifndef RT_QW_LANES
+#define RT_QW_LANES 32
 #endif
 // the queue kernel walks the 64-byte nodes (BvhNodeH) when the scene has them
 #ifndef RT_QNODE_H
@@ -2542,15 +2550,22 @@ void render_kernel_q(const KParams kp)
                 const Ray32 r32 = ray32<QB == 3 && !OPQ>(kp, L.o, dd);
                 unsigned short* stk = bvh_stack_q<QB, OPQ>();
                 const QNode* top = NTOP > 0 ? bvh_top_q<QNode, NTOP>() : nullptr;
+                // deep trees (QB 3): at least RT_QW_MIN visits, then more while at
+                // least RT_QW_LANES lanes of the wave are still walking, up to
+                // RT_QW_MAX (long walks -- e.g. rays skimming RTX_MAP/nature's
+                // terrain -- finish in fewer rounds, short ones hand the wave back
+                // to the path work as before)
+                constexpr int JMIN = QB == 3 ? RT_QW_MIN : QB, JMAX = QB == 3 ? RT_QW_MAX : QB;
 #pragma unroll 1
-                for (int j = 0; j < (QB == 3 && !OPQ ? RT_QN_STEPS : QB); ++j) {
+                for (int j = 0; j < JMAX; ++j) {
                     if (L.state == SM_TRAV) {
                         Cnt cnt;
                         if (!bvh_step<false, false, NTOP, HN>(kp, L.o, dd, r32, stk, node, sp, L.best, L.kind, L.win,
                                                            win_orig, cnt, top))
                             L.state = SM_RESOLVE;
                     }
-                    if (__ballot(L.state == SM_TRAV) == 0ull) break;
+                    const unsigned long long wm = __ballot(L.state == SM_TRAV);
+                    if (wm == 0ull || (j + 1 >= JMIN && __popcll(wm) < RT_QW_LANES)) break;
                 }
 #if RT_WALK_PRIO
                 __builtin_amdgcn_s_setprio(0);
