@@ -164,6 +164,7 @@ __device__ __forceinline__ V3 mulv(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y,
 __device__ __forceinline__ V3 muls(V3 a, double t) { return v3(a.x * t, a.y * t, a.z * t); }
 __device__ __forceinline__ V3 divs(V3 a, double t) { return v3(a.x / t, a.y / t, a.z / t); }
 __device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
 __device__ __forceinline__ V3 cross(V3 u, V3 v)
 {
     return v3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
@@ -1159,12 +1160,23 @@ __device__ __forceinline__ void sky_material(const KParams& kp, int idx, const S
     mat.alpha = 1.0;
 }
 
+// randomDouble(-0.5, 0.5) and randomDouble(0, 1) of one 31-bit draw r
+// (rtutility.h:229-231: min + (max - min) * (r / 2^31)): r / 2^31 and the
+// product by 1 are exact, so the result is ONE rounding of r 2^-31 - 0.5, i.e.
+// fma(r, 2^-31, -0.5), and r 2^-31 itself for [0, 1) (0.0 + u == u for u >= 0)
+__device__ __forceinline__ double rand_m05(uint32_t r) { return fma((double)r, 0x1p-31, -0.5); }
+__device__ __forceinline__ double rand_01(uint32_t r) { return (double)r * 0x1p-31; }
+
 // random_dir_no_norm's vector before its normalize, rtutility.h:192-200
-// (float sinf/cosf of double args), from its two draws u, v
-__device__ __forceinline__ V3 sampler_vec(double u, double v)
+// (float sinf/cosf of double args), from its two 31-bit draws ru, rv:
+// u = ru / 2^31 and v = rv / 2^31 are exact, so 2 PI u = ru (2 PI 2^-31)
+// (one rounding of the same product) and 2 v - 1 = fma(rv, 2^-30, -1) (2 v
+// exact, one rounding of the difference): the reference's values in three
+// VALU fewer
+__device__ __forceinline__ V3 sampler_vec(uint32_t ru, uint32_t rv)
 {
-    const double theta = 0x1.921fb54442d18p+2 * u;        // 2*PI*u
-    const double xv = 2 * v - 1;                          // phi = acos(2v - 1): only (float)phi is used
+    const double theta = (double)ru * 0x1.921fb54442d18p-29;      // 2*PI*u
+    const double xv = fma((double)rv, 0x1p-30, -1.0);              // phi = acos(2v - 1): only (float)phi is used
     float st_, ct_, sp_, cp_;
     if (!phi_sincosf_fast(xv, sp_, cp_)) {                // uncertain rounding (~1e-4): full path
         const double phi = pm_acos(xv);
@@ -1179,9 +1191,9 @@ template <bool COUNT>
 __device__ __forceinline__ V3 random_dir(Stream& st, Cnt& cnt)
 {
     if (COUNT) cnt.c[RT_CNT_SHADE] += 1;
-    const double u = unit31(st.next31());
-    const double v = unit31(st.next31());
-    const V3 dir = sampler_vec(u, v);
+    const uint32_t ru = st.next31();
+    const uint32_t rv = st.next31();
+    const V3 dir = sampler_vec(ru, rv);
     return normalize_unit(dir);
 }
 
@@ -1372,10 +1384,10 @@ struct CamDraws {
 template <bool CU, class ST>
 __device__ __forceinline__ void camera_ray(const KParams& kp, int x, int g, ST& st, V3& no, V3& rd)
 {
-    const double ju = -0.5 + 1.0 * unit31(st.next31());     // randomDouble(-0.5, 0.5)
-    const double jv = -0.5 + 1.0 * unit31(st.next31());
-    const double jx = -0.5 + 1.0 * unit31(st.next31());
-    const double jy = -0.5 + 1.0 * unit31(st.next31());
+    const double ju = rand_m05(st.next31());     // randomDouble(-0.5, 0.5)
+    const double jv = rand_m05(st.next31());
+    const double jx = rand_m05(st.next31());
+    const double jy = rand_m05(st.next31());
     const int b = opq0();
     const cdptr U = (cdptr)kp.uni;
     // main.c:265-266; main_cuda.cu:152-153 adds 0.5 first
@@ -1542,7 +1554,7 @@ struct LanePath {
                             top_n2 = mat.ior;
                         }
                         const V3 refr = refracted(d, nn, n1, n2);
-                        const double rnd = 0.0 + 1.0 * unit31(st.next31());
+                        const double rnd = rand_01(st.next31());
                         if (rnd > mat.alpha) {
                             d = refr;
                             shade = false;
@@ -2397,7 +2409,7 @@ struct QPath {
             }
             const V3 rf = refracted(d, nn, n1, n2);
             // (RT_REFR_PREFETCH) the draw is in the block cache whatever its slot
-            const double rnd = 0.0 + 1.0 * unit31(RT_REFR_PREFETCH ? st.next31_cached() : st.next31());
+            const double rnd = rand_01(RT_REFR_PREFETCH ? st.next31_cached() : st.next31());
             if (rnd > mat.alpha) {
                 d = rf;
                 shaded = false;
@@ -2760,8 +2772,8 @@ void render_kernel_q(const KParams kp)
             V3 no = v3(0, 0, 0);
             if (cam) {
                 CamDraws w{blk, 0};
-                const double ju = -0.5 + 1.0 * unit31(w.next31());     // randomDouble(-0.5, 0.5)
-                const double jv = -0.5 + 1.0 * unit31(w.next31());
+                const double ju = rand_m05(w.next31());     // randomDouble(-0.5, 0.5)
+                const double jv = rand_m05(w.next31());
                 const int b = opq0();
                 const cdptr U = (cdptr)kp.uni;
                 const double nu = (double)x + ju, nv = (double)g + jv;
@@ -2777,17 +2789,15 @@ void render_kernel_q(const KParams kp)
                 if (kp.cam_pin) {                              // zero aperture: the origin itself (host-checked)
                     no = co;
                 } else {
-                    const double jx = -0.5 + 1.0 * unit31(w.next31());
-                    const double jy = -0.5 + 1.0 * unit31(w.next31());
+                    const double jx = rand_m05(w.next31());
+                    const double jy = rand_m05(w.next31());
                     const double dx = jx * U[b + U_OX], dy = jy * U[b + U_OY];
                     no = co + v3(dx, dy, 0);
                 }
                 X = dest - no;
             } else {
                 // random_dir_no_norm (rtutility.h:189-203), then n + dir (main.c:163)
-                const double u = unit31(wa >> 1);
-                const double v = unit31(wb >> 1);
-                X = H.hn + normalize_unit(sampler_vec(u, v));
+                X = H.hn + normalize_unit(sampler_vec(wa >> 1, wb >> 1));
                 st.n += aor ? 0u : pbr ? 4u : 2u;
             }
             const V3 dn = normalize(X);
@@ -3290,7 +3300,7 @@ __global__ __launch_bounds__(256) void verify_normalize_kernel(unsigned long lon
         const uint32_t cls = q.w2 & 7u;
         V3 got;
         if (cls >= 4u) {                            // the sampler's unit vectors
-            a = sampler_vec(unit31(p.w0 >> 1), unit31(p.w1 >> 1));
+            a = sampler_vec(p.w0 >> 1, p.w1 >> 1);
             fp = true;
             got = normalize_unit(a);
         } else {
