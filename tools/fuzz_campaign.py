@@ -1,7 +1,9 @@
-"""GPU-vs-oracle fuzz campaign on seeds the test suite does not use: the four
-families of tests/test_gpu_fuzz.py (random scenes; exact-zero colours on the
-queue kernel; CUDA semantics; 100-400 triangle BVH scenes on a 1-3 block
-queue grid), bit for bit (check_parity: canva, albedo, normal, radiance).
+"""GPU-vs-oracle fuzz campaign on seeds the test suite does not use: the
+families of tests/test_gpu_fuzz.py (random scenes with 0-24 bounces; exact-zero
+colours on the queue kernel; CUDA semantics; 100-400 triangle BVH scenes on a
+1-3 block queue grid; the opaque instantiations; r06: main()'s far coordinate
+regime, with and without 100-400 triangle trees), bit for bit (check_parity:
+canva, albedo, normal, radiance).
 Prints one line per scene; writes a JSON summary.
 Usage: python3 tools/fuzz_campaign.py OUT.json [scenes per family] [first seed]"""
 import json
@@ -43,6 +45,12 @@ def family_cases(name, seed):
                                  spp=40 + 8 * (seed % 2))
         p.largeur_image, p.hauteur_image = min(p.largeur_image, 20), min(p.hauteur_image, 15)
         return (bundle, p), str(1 + seed % 3)
+    if name == "far_scale":                    # r06: main()'s coordinate regime, odd seeds zero exit off
+        return random_scene(seed, far=True), None
+    if name == "far_bvh_queue":                # r06: far regime with 100-400 triangle trees
+        bundle, p = random_scene(seed, far=True, chunks=4 + seed % 3, nt_range=(100, 400), spp=24)
+        p.largeur_image, p.hauteur_image = min(p.largeur_image, 24), min(p.hauteur_image, 18)
+        return (bundle, p), None
     raise ValueError(name)
 
 
@@ -51,7 +59,7 @@ def main():
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     first = int(sys.argv[3]) if len(sys.argv) > 3 else 10000
     fams = os.environ.get("FUZZ_FAMILIES", "random,zero_throughput_queue,cuda_semantics,bvh_queue_tiny_grid,"
-                          "opaque_spheres_queue,opaque_bvh_queue_tiny_grid").split(",")
+                          "opaque_spheres_queue,opaque_bvh_queue_tiny_grid,far_scale,far_bvh_queue").split(",")
     res = {"families": {}, "first_seed": first, "scenes_per_family": n, "failures": []}
     t0 = time.time()
     for fi, fam in enumerate(fams):
@@ -64,7 +72,11 @@ def main():
             else:
                 os.environ["RT_QUEUE_BLOCKS"] = blocks
             try:
-                check_parity(bundle, p)
+                if fam.startswith("far") and seed % 2:
+                    with tipe_rt.reference_counts():       # paths continue after sky hits
+                        check_parity(bundle, p)
+                else:
+                    check_parity(bundle, p)
                 ok += 1
                 status = "ok"
             except AssertionError as e:
