@@ -94,6 +94,9 @@ static_assert(RT_CAND_M * RT_CAND_M * RT_CAND_T1 >= 0x1.8p-89 && RT_CAND_M <= 0x
 #ifndef RT_TRI_BF                   // brute-force triangle scan without branches (r04: C3 +1.3 %, C5 +1.3 %)
 #define RT_TRI_BF 1
 #endif
+#ifndef RT_WAVES_PER_SIMD_Q4        // occupancy bound of the shallow-tree queue kernel (A/B knob)
+#define RT_WAVES_PER_SIMD_Q4 RT_WAVES_PER_SIMD_Q
+#endif
 #ifndef RT_WAVES_PER_SIMD_QS        // occupancy bound of the sphere-only queue kernel (A/B knob)
 #define RT_WAVES_PER_SIMD_QS RT_WAVES_PER_SIMD_Q
 #endif
@@ -2470,7 +2473,9 @@ __device__ __forceinline__ void decode_task(KParamsK K, unsigned t, uint32_t e[k
 }
 
 template <bool SKY, int AOM, int QB, bool OPQ = false>   // OPQ: (BVH scenes) every material opaque
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QB < 0 ? RT_WAVES_PER_SIMD_QS : RT_WAVES_PER_SIMD_Q)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(QB < 0 ? RT_WAVES_PER_SIMD_QS
+                                                                     : QB == 4 ? RT_WAVES_PER_SIMD_Q4
+                                                                               : RT_WAVES_PER_SIMD_Q)))
 void render_kernel_q(const KParams kp)
 {
     // incomingLight / rayColor in LDS: both for the non-BVH kernels, incomingLight
