@@ -888,11 +888,35 @@ __device__ __forceinline__ void box4h(const KParams& kp, const BvhNodeH* nd, uin
 // the next node (nearest hit internal child, else the stack top).  Returns
 // false when the traversal is over.  tris_bvh loops it to the end; the
 // resumable trace (render_sm) runs a bounded number of visits per round.
+#ifndef RT_DIAG_STALE                // diagnostic build: COUNT walks count visits to nodes whose entry
+#define RT_DIAG_STALE 0              // distance already exceeds the cull distance (in the stack-over slot;
+#endif                               // stack entries below depth 16 only)
+__device__ __forceinline__ float* diag_lds()
+{
+    __shared__ float dg_lds[RT_DIAG_STALE ? 17 * 256 : 1];
+    return dg_lds + threadIdx.x;
+}
+__device__ __forceinline__ unsigned* diag_cnt()
+{
+    __shared__ unsigned dc_lds[RT_DIAG_STALE == 2 ? 2 * 256 : 1];
+    return dc_lds + threadIdx.x;
+}
 template <bool COUNT, bool CU, int NTOP = 0, bool H = false>
 __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3 d, const Ray32& r32,
                                          unsigned short* stk, int& node, int& sp, double& best, int& kind,
                                          int& win, int& win_orig, Cnt& cnt, const void* top = nullptr)
 {
+    if constexpr (RT_DIAG_STALE && (COUNT || RT_DIAG_STALE == 2)) {
+        float* dg = diag_lds();
+        if (node == 0) dg[16 * 256] = -__builtin_huge_valf();          // the root: a new walk
+        const bool stale = dg[16 * 256] > cull32(kp, best);
+        if (COUNT && stale) cnt.c[RT_CNT_BVH_STACK_OVER] += 1;
+        if (!COUNT) {                                                  // queue kernel: per-lane sums
+            unsigned* dc = diag_cnt();
+            dc[0] += 1u;
+            dc[256] += stale ? 1u : 0u;
+        }
+    }
     // NTOP > 0: the first NTOP nodes (breadth-first: the top levels) are read
     // from the block's LDS copy `top`, the rest from HBM/L2; H: 64-byte nodes
     if (COUNT) {
@@ -923,16 +947,20 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
             tnext = tn[c];
         } else {
             int push = ch;
+            float tpush = tn[c];
             if (tn[c] < tnext) {                         // nearer: enter it, push the previous pick
                 push = next;
+                tpush = tnext;
                 next = ch;
                 tnext = tn[c];
             }
-            if (COUNT && sp >= kp.stack_cap) cnt.c[RT_CNT_BVH_STACK_OVER] += 1;
+            if (!RT_DIAG_STALE && COUNT && sp >= kp.stack_cap) cnt.c[RT_CNT_BVH_STACK_OVER] += 1;
             if (!COUNT || sp < kStack4) {    // COUNT walks use the fixed grid's stack
+                if (RT_DIAG_STALE && (COUNT || RT_DIAG_STALE == 2) && sp < 16) diag_lds()[sp * 256] = tpush;
                 stk[sp * 256] = (unsigned short)push;
                 ++sp;
             }
+            (void)tpush;
         }
     }
     // The triangles of every hit leaf in one loop, one triangle per lane and
@@ -953,11 +981,14 @@ __device__ __forceinline__ bool bvh_step(const KParams& kp, const V3 o, const V3
     }
     if (next >= 0) {
         node = next;
+        if (RT_DIAG_STALE && (COUNT || RT_DIAG_STALE == 2)) diag_lds()[16 * 256] = tnext;
         return true;
     }
     if (sp == 0) return false;
     --sp;
     node = stk[sp * 256];
+    if (RT_DIAG_STALE && (COUNT || RT_DIAG_STALE == 2))
+        diag_lds()[16 * 256] = sp < 16 ? diag_lds()[sp * 256] : -__builtin_huge_valf();
     return true;
 }
 
@@ -2500,6 +2531,10 @@ void render_kernel_q(const KParams kp)
     L.pkw = 0;
     L.prs = 0.0;
     L.state = SM_CAM;                // s = 0 >= s1 = 0: takes a task first
+#if RT_DIAG_STALE == 2
+    diag_cnt()[0] = 0u;
+    diag_cnt()[256] = 0u;
+#endif
     int x = 0, g = 0, s1 = 0;
     int node = 0, sp = 0, win_orig = 0;      // BVH walk in flight (state SM_TRAV)
     unsigned chunk = 0, p = 0, pixel = 0;
@@ -2839,6 +2874,10 @@ void render_kernel_q(const KParams kp)
         q[1] = (unsigned long long)wall_clock64();
         q[2] = rounds;
         q[3] = ntasks;
+#if RT_DIAG_STALE == 2
+        q[2] = diag_cnt()[0];        // diagnostic: node visits and stale visits of the lane
+        q[3] = diag_cnt()[256];
+#endif
 #if RT_PHASE_CLOCK
         for (int k = 0; k < 5; ++k) q[4 + k] = ph[k];
 #endif
