@@ -44,6 +44,7 @@ def test_host_h_symbols_exported():
 def test_library_loads_and_reports_version():
     L = tipe_rt.lib()
     assert b"gfx950" in L.rt_version()
+    assert b"(abi %d," % L.rt_abi_version() in L.rt_version()       # the string names the ABI it exports
     p = T.Params()
     L.rt_params_init(C.byref(p))
     assert p.rng == T.RT_RNG_PHILOX and p.seed == 1010 and p.compat_int_truncation == 1 and p.spp_chunks == T.RT_SPP_CHUNKS_AUTO

@@ -749,9 +749,14 @@ const char* rt_last_render_kernel(void) { return last_render_kernel(); }
 
 const char* rt_version(void)
 {
-    return "tipe-raytracer-mi355x 0.5 (abi 3, gfx950; precision FP64, bit-exact against the reference's own "
-           "composition; RT_PREC_FP32 removed (RT_EUNSUPPORTED); rt_params_init defaults spp_chunks to "
-           "RT_SPP_CHUNKS_AUTO, a fixed per-pixel slice grouping)";
+#define RT_STR2(x) #x
+#define RT_STR(x) RT_STR2(x)
+    return "tipe-raytracer-mi355x 0.6 (abi " RT_STR(RT_ABI_VERSION) ", gfx950; precision FP64, bit-exact against "
+           "the reference's own composition; RT_PREC_FP32 removed (RT_EUNSUPPORTED); rt_params_init defaults "
+           "spp_chunks to RT_SPP_CHUNKS_AUTO, a fixed per-pixel slice grouping; multi-device gathers over RCCL "
+           "(RT_GATHER_RCCL) or peer copies (RT_GATHER_PEER))";
+#undef RT_STR
+#undef RT_STR2
 }
 
 int rt_device_count(void)
